@@ -1,0 +1,172 @@
+"""TEST INFRASTRUCTURE ONLY -- the oracle.
+
+ctypes bindings for
+  * ``oracle/libqpsk_cpu.so``  -- clean-room C restatement of the reference RX
+    path (``oracle/cpu_ref.c``), plus the TX restatement used for synthesis;
+  * ``oracle/_ref/libqpsk_ref.so`` -- the UNMODIFIED reference sources compiled
+    from /root/reference by ``oracle/Makefile`` (present in the build container
+    and shipped prebuilt to the GPU box; never required).
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s cpu_baseline leg
+import this package, and only as the checker / baseline -- the product path
+(``singlecarrier_amd``) never touches it.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+FRAME = 1880
+NBITS = 62
+NDSYM = 31
+
+TRACE_DTYPE = np.dtype([("max_index", "<i4"), ("matches", "<i4"), ("valid", "<i4"),
+                        ("rx_timing", "<i4"), ("soft", "<f4", (31, 2))])
+REF_TRACE_DTYPE = np.dtype([("max_index", "<i4"), ("matches", "<i4"), ("valid", "<i4"),
+                            ("rx_timing", "<i4"), ("soft", "<f4", (31, 2)),
+                            ("raw_dibit", "u1", (31,)), ("pad", "u1", (1,))])
+assert TRACE_DTYPE.itemsize == 264 and REF_TRACE_DTYPE.itemsize == 296
+
+_cpu = None
+_ref = None
+
+
+def build(ref: bool = True) -> None:
+    """Compile the restatement (always) and the reference harness (when the
+    reference tree is present).  Building the checker is not using it."""
+    subprocess.run(["make", "-s", "-C", HERE, "cpu"], check=True)
+    if ref and os.path.isdir("/root/reference/src"):
+        subprocess.run(["make", "-s", "-C", HERE, "ref"], check=True)
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p) if a is not None else None
+
+
+def cpu_lib():
+    global _cpu
+    if _cpu is None:
+        path = os.path.join(HERE, "libqpsk_cpu.so")
+        if not os.path.exists(path):
+            build(ref=False)
+        lib = C.CDLL(path)
+        lib.qc_rx_batch.restype = C.c_long
+        lib.qc_rx_batch.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
+                                    C.c_void_p, C.c_int]
+        lib.qc_synth_batch.restype = None
+        lib.qc_synth_batch.argtypes = [C.c_uint64, C.c_uint32, C.c_int, C.c_double,
+                                       C.c_void_p, C.c_long, C.c_int]
+        lib.qc_mixer_table.argtypes = [C.c_void_p]
+        lib.qc_keystream.argtypes = [C.c_void_p, C.c_int]
+        _cpu = lib
+    return _cpu
+
+
+def ref_available() -> bool:
+    return os.path.exists(os.path.join(HERE, "_ref", "libqpsk_ref.so"))
+
+
+def ref_lib():
+    global _ref
+    if _ref is None:
+        lib = C.CDLL(os.path.join(HERE, "_ref", "libqpsk_ref.so"))
+        lib.ref_rx_stream.restype = C.c_int
+        lib.ref_rx_stream.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
+        lib.ref_rx_batch.restype = C.c_int
+        lib.ref_rx_batch.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+        lib.ref_layout_gap.restype = C.c_long
+        lib.ref_log_set.argtypes = [C.c_void_p, C.c_size_t]
+        _ref = lib
+    return _ref
+
+
+def _frames(x):
+    x = np.ascontiguousarray(x, dtype=np.int16)
+    if x.ndim == 2:
+        x = x[None]
+    assert x.ndim == 3 and x.shape[2] == FRAME
+    return x
+
+
+def cpu_rx(x, threads: int = 0, trace: bool = False):
+    """Restatement over x [nch][nframes][1880] (or [nframes][1880]).
+    Returns bits [nch][nframes][62] u8, valid [nch][nframes] u8, trace|None."""
+    x = _frames(x)
+    nch, nf, _ = x.shape
+    bits = np.zeros((nch, nf, NBITS), np.uint8)
+    valid = np.zeros((nch, nf), np.uint8)
+    tr = np.zeros((nch, nf), TRACE_DTYPE) if trace else None
+    threads = threads or min(16, os.cpu_count() or 1)
+    cpu_lib().qc_rx_batch(_p(x), nch, nf, _p(bits), _p(valid), _p(tr), threads)
+    return bits, valid, tr
+
+
+def ref_rx(x, trace: bool = False, log: bool = False):
+    """The unmodified reference, one channel at a time (single thread)."""
+    x = _frames(x)
+    nch, nf, _ = x.shape
+    lib = ref_lib()
+    bits = np.zeros((nch, nf, NBITS), np.uint8)
+    valid = np.zeros((nch, nf), np.uint8)
+    tr = np.zeros((nch, nf), REF_TRACE_DTYPE) if trace else None
+    buf = C.create_string_buffer(1 << 20) if log else None
+    if log:
+        lib.ref_log_set(buf, len(buf))
+    for c in range(nch):
+        r = lib.ref_rx_stream(_p(x[c]), nf, _p(bits[c]), _p(valid[c]),
+                              _p(tr[c]) if trace else None)
+        if r < 0:
+            raise RuntimeError("reference static layout is not model A")
+    if log:
+        lib.ref_log_set(None, 0)
+    return (bits, valid, tr, buf.value.decode()) if log else (bits, valid, tr)
+
+
+def ref_stages(x):
+    """One channel through the reference, frame by frame, returning the
+    reference's own buffers after each call: dec [nf][290][2] (decimated_frame
+    [0..289]) and mixed [nf][1880][2] (input_frame[1880..3759])."""
+    x = _frames(x)[0]
+    nf = x.shape[0]
+    lib = ref_lib()
+    lib.ref_rx_reset.restype = C.c_int
+    lib.ref_rx_frame.restype = C.c_int
+    lib.ref_rx_frame.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    lib.ref_peek_dec.argtypes = [C.c_void_p]
+    lib.ref_peek_mixed.argtypes = [C.c_void_p]
+    if lib.ref_rx_reset() != 0:
+        raise RuntimeError("reference static layout is not model A")
+    dec = np.zeros((nf, 290, 2), np.float32)
+    mixed = np.zeros((nf, FRAME, 2), np.float32)
+    bits = np.zeros((nf, NBITS), np.uint8)
+    valid = np.zeros(nf, np.uint8)
+    for n in range(nf):
+        valid[n] = lib.ref_rx_frame(_p(x[n]), _p(bits[n]), None)
+        lib.ref_peek_dec(_p(dec[n]))
+        lib.ref_peek_mixed(_p(mixed[n]))
+    return dec, mixed, bits, valid
+
+
+def synth(seed: int, nch: int, nframes: int, ebn0_db: float = 1000.0, c0: int = 0,
+          threads: int = 0) -> np.ndarray:
+    """Synthetic channel streams [nch][nframes][1880] int16."""
+    out = np.empty((nch, nframes, FRAME), np.int16)
+    threads = threads or min(16, os.cpu_count() or 1)
+    cpu_lib().qc_synth_batch(seed, c0, nch, float(ebn0_db), _p(out), nframes * FRAME, threads)
+    return out
+
+
+def mixer_table() -> np.ndarray:
+    p = np.zeros((FRAME, 2), np.float32)
+    cpu_lib().qc_mixer_table(_p(p))
+    return p
+
+
+def keystream(n: int) -> np.ndarray:
+    ks = np.zeros(n, np.uint8)
+    cpu_lib().qc_keystream(_p(ks), n)
+    return ks

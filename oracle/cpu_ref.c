@@ -1,0 +1,532 @@
+/*
+ * cpu_ref.c -- TEST INFRASTRUCTURE ONLY (oracle): clean-room C restatement of
+ * the reference receive path, see cpu_ref.h.
+ *
+ * Arithmetic contract: IEEE fp32, round-to-nearest, every
+ * product and sum rounded separately (built with -ffp-contract=off), sums in
+ * the reference's index order starting from 0.0f, complex products written out
+ * as (ac - bd, ad + bc) exactly as gcc expands them for finite operands.
+ *
+ * Minimal form, each step proved equal to the reference:
+ *  - mixer: frame n uses (-1)^n * P[t] (A.2), P[t] = R^(t+1) by the fp32
+ *    recurrence of src/qpsk.c:139; the per-frame renormalisation
+ *    (src/qpsk.c:147) maps P[1879] to exactly -1+0i, so the phase alternates.
+ *  - FIR (src/fir.c:22-44): call n filters the PREVIOUS frame's mixed samples
+ *    (input_frame[0..1879] holds them, src/qpsk.c:143); only outputs
+ *    [0..101] and {5i+rt} are observable (A.6) and only those are computed.
+ *  - decimation with the gcc -O2 overflow semantics ("model A", A.4):
+ *    dec[0..187] = D_{n-1}, dec[188..] = fir_out_n[0..], D_n[i] = fir_out_n[5i+rt].
+ *  - correlator (src/qpsk.c:88-96): preamble symbols are p+pj with p = +-1, so
+ *    each product is p*(dr-di, di+dr) exactly (A.3).
+ *  - invalid frames skip data_eq (unobservable, A.6) but advance the keystream
+ *    by 62 bits, i.e. frame n always uses keystream bits [62n, 62n+62).
+ */
+#include "cpu_ref.h"
+
+#include <math.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* src/constants.c:25-42 (preamblevalues) */
+static const int8_t k_pre[QC_PRE] = {
+    -1, 1, 1, -1, -1, 1, 1, 1, -1, 1, -1, -1, 1, 1, -1, -1,
+    1, 1, -1, 1, -1, -1, 1, -1, 1, -1, 1, -1, 1, -1, 1, 1,
+    1, -1, 1, 1, 1, 1, -1, -1, 1, -1, -1, 1, 1, -1, 1, -1,
+    1, 1, -1, 1, -1, -1, 1, -1, -1, -1, -1, 1, 1, -1, 1, -1,
+    1, 1, 1, -1, -1, 1, 1, -1, 1, 1, -1, -1, 1, 1, -1, 1,
+    1, -1, 1, 1, -1, -1, -1, 1, -1, 1, -1, 1, -1, -1, -1, 1,
+    -1, -1, 1, -1, 1, 1, -1, -1, -1, -1, -1, 1, 1, 1, -1, 1,
+    1, -1, 1, 1, -1, -1, 1, 1, -1, 1, -1, 1, -1, -1, -1, 1};
+
+/* src/constants.c:106-156 (alpha35_root; rx uses it, firwide=false src/qpsk.c:60) */
+static const float k_rrc[QC_NTAPS] = {
+    -0.00024537f, -0.00220636f, -0.00291493f, -0.00175708f, 0.00068764f,
+    0.00282391f,  0.00297883f,  0.00059170f,  -0.00311265f, -0.00553670f,
+    -0.00418297f, 0.00153693f,  0.00925400f,  0.01422443f,  0.01161151f,
+    -0.00045943f, -0.01864749f, -0.03439334f, -0.03667604f, -0.01667595f,
+    0.02761997f,  0.08908617f,  0.15279058f,  0.20079911f,  0.21864582f,
+    0.20079911f,  0.15279058f,  0.08908617f,  0.02761997f,  -0.01667595f,
+    -0.03667604f, -0.03439334f, -0.01864749f, -0.00045943f, 0.01161151f,
+    0.01422443f,  0.00925400f,  0.00153693f,  -0.00418297f, -0.00553670f,
+    -0.00311265f, 0.00059170f,  0.00297883f,  0.00282391f,  0.00068764f,
+    -0.00175708f, -0.00291493f, -0.00220636f, -0.00024537f};
+
+#define GAIN_F 2.2f    /* headers/fir.h:17 */
+#define KAL_E 0.1f     /* src/kalman.c:61  */
+#define KAL_Q 0.08f    /* src/kalman.c:62  */
+
+static float bits2f(uint32_t u) {
+    float f;
+    memcpy(&f, &u, 4);
+    return f;
+}
+
+/* ------------------------------------------------------------------ tables */
+
+static float g_p[QC_FRAME][2];       /* mixer table P[t] * 2^-14 */
+static uint8_t g_ks[32767 + 64];     /* RX keystream, one period + slack */
+static pthread_once_t g_once = PTHREAD_ONCE_INIT;
+
+/* fbb_rx_rect = cmplx(TAU*(-CENTER+FOFFSET)/FS), src/qpsk.c:428; the bits of
+ * glibc's cosf/sinf at that float argument (pinned by test_oracle.py). */
+static void rx_rect(float r[2]) {
+    r[0] = bits2f(0x3f26423au);
+    r[1] = bits2f(0xbf42a9f7u);
+}
+
+void qc_mixer_table(float p[QC_FRAME][2]) {
+    float r[2], ph[2] = {1.0f, 0.0f};  /* fbb_rx_phase = cmplx(0) src/qpsk.c:427 */
+    rx_rect(r);
+    for (int t = 0; t < QC_FRAME; t++) { /* fbb_rx_phase *= fbb_rx_rect :139 */
+        float a = ph[0] * r[0] - ph[1] * r[1];
+        float b = ph[0] * r[1] + ph[1] * r[0];
+        ph[0] = a;
+        ph[1] = b;
+        p[t][0] = a;
+        p[t][1] = b;
+    }
+}
+
+void qc_keystream(uint8_t *ks, int n) {
+    uint16_t m = 0x4A80; /* SEED headers/scramble.h:16 */
+    for (int k = 0; k < n; k++) { /* scramble_internal, src/scramble.c:57-69 */
+        uint16_t o = (uint16_t)(((m & 0x2) >> 1) ^ (m & 0x1));
+        ks[k] = (uint8_t)o;
+        m = (uint16_t)((m >> 1) | (o << 14));
+    }
+}
+
+static void init_tables(void) {
+    float p[QC_FRAME][2];
+    qc_mixer_table(p);
+    for (int t = 0; t < QC_FRAME; t++) {  /* (float)in/16384 folded into P: exact */
+        g_p[t][0] = p[t][0] * 0x1p-14f;
+        g_p[t][1] = p[t][1] * 0x1p-14f;
+    }
+    qc_keystream(g_ks, (int)sizeof g_ks);
+}
+
+/* ------------------------------------------------------------------ RX */
+
+void qc_chan_init(qc_chan_t *ch) {
+    pthread_once(&g_once, init_tables);
+    memset(ch, 0, sizeof(*ch));
+    ch->rx_timing = 3;  /* FINE_TIMING_OFFSET, headers/qpsk_internal.h:23 */
+}
+
+/* mixed sample m_k[t] (src/qpsk.c:139-144) of frame k with parity sign */
+static inline void mix(const int16_t *x, uint32_t k, int t, float out[2]) {
+    float v = (float)x[t];
+    float pr = g_p[t][0], pi = g_p[t][1];
+    if (k & 1u) {
+        pr = -pr;
+        pi = -pi;
+    }
+    out[0] = pr * v;
+    out[1] = pi * v;
+}
+
+/* one RRC output (src/fir.c:36-42): M points at the sample aligned with tap 0 */
+static inline void fir_at(const float (*M)[2], float out[2]) {
+    float yr = 0.0f, yi = 0.0f;
+    for (int i = 0; i < QC_NTAPS; i++) {
+        yr = yr + M[i][0] * k_rrc[i];
+        yi = yi + M[i][1] * k_rrc[i];
+    }
+    out[0] = yr * GAIN_F;
+    out[1] = yi * GAIN_F;
+}
+
+typedef struct {
+    float eq[5][2];          /* eq_coeff   src/kalman.c:19 */
+    float g[5][2];           /* kalman_gain src/kalman.c:20 */
+    float u[5][5][2];        /* src/kalman.c:25 */
+    float d[5];              /* src/kalman.c:29 */
+    float y;                 /* kalman_y */
+} kal_t;
+
+static void kal_reset(kal_t *k) {  /* kalman_reset, src/kalman.c:42-55 */
+    memset(k, 0, sizeof(*k));
+    for (int i = 0; i < 5; i++) k->d[i] = 1.0f;
+}
+
+/* kalman_calculate, src/kalman.c:85-141, on x[0..4] = dec[index..index+4] */
+static void kal_calc(kal_t *k, const float (*x)[2]) {
+    float f[5][2], a[5];
+    const float E = KAL_E, q = KAL_Q;
+    f[0][0] = x[0][0];                         /* 6.2 f0 = conj(x0) */
+    f[0][1] = -x[0][1];
+    for (int j = 1; j < 5; j++) {
+        /* u0j*conj(x0) + conj(xj): the double-precision conj() sum rounds to
+         * the fp32 sum (2p+2 <= 53), so it is an fp32 add. */
+        float ur = k->u[0][j][0], ui = k->u[0][j][1];
+        float cr = x[0][0], ci = -x[0][1];
+        float pr = ur * cr - ui * ci;
+        float pi = ur * ci + ui * cr;
+        f[j][0] = pr + x[j][0];
+        f[j][1] = pi + (-x[j][1]);
+        for (int i = 1; i < j; i++) {
+            ur = k->u[i][j][0];
+            ui = k->u[i][j][1];
+            cr = x[i][0];
+            ci = -x[i][1];
+            pr = ur * cr - ui * ci;
+            pi = ur * ci + ui * cr;
+            f[j][0] = f[j][0] + pr;
+            f[j][1] = f[j][1] + pi;
+        }
+    }
+    for (int j = 0; j < 5; j++) {              /* 6.4 g = f*d */
+        k->g[j][0] = f[j][0] * k->d[j];
+        k->g[j][1] = f[j][1] * k->d[j];
+    }
+    /* 6.5/6.6 a_j = a_{j-1} + Re(g_j * conj(f_j)) */
+    a[0] = E + (k->g[0][0] * f[0][0] - k->g[0][1] * (-f[0][1]));
+    for (int j = 1; j < 5; j++)
+        a[j] = a[j - 1] + (k->g[j][0] * f[j][0] - k->g[j][1] * (-f[j][1]));
+    const float hq = 1.0f + q;                 /* 6.7 */
+    const float ht = a[4] * q;
+    float y = 1.0f / (a[0] + ht);              /* 6.19 */
+    k->d[0] = k->d[0] * ((hq * (E + ht)) * y); /* 6.20 */
+    for (int j = 1; j < 5; j++) {
+        float B = a[j - 1] + ht;               /* 6.21 */
+        float hr = (-f[j][0]) * y;             /* 6.11 h = -f*y */
+        float hi = (-f[j][1]) * y;
+        y = 1.0f / (a[j] + ht);                /* 6.22 */
+        k->d[j] = k->d[j] * ((hq * B) * y);    /* 6.13 */
+        for (int i = 0; i < j; i++) {
+            float b1r = k->u[i][j][0], b1i = k->u[i][j][1];
+            float gr = k->g[i][0], gi = -k->g[i][1];       /* conj(g_i) */
+            k->u[i][j][0] = b1r + (hr * gr - hi * gi);     /* 6.15 */
+            k->u[i][j][1] = b1i + (hr * gi + hi * gr);
+            float jr = k->g[j][0], ji = k->g[j][1];
+            float cr = b1r, ci = -b1i;                     /* conj(B1) */
+            k->g[i][0] = k->g[i][0] + (jr * cr - ji * ci); /* 6.16 */
+            k->g[i][1] = k->g[i][1] + (jr * ci + ji * cr);
+        }
+    }
+    k->y = y;
+}
+
+/* update_eq, src/equalizer.c:25-40 */
+static void update_eq(kal_t *k, const float (*x)[2], float er, float ei) {
+    kal_calc(k, x);
+    er = er * k->y;
+    ei = ei * k->y;
+    for (int i = 0; i < 5; i++) {
+        float gr = k->g[i][0], gi = -k->g[i][1];
+        k->eq[i][0] = k->eq[i][0] + (er * gr - ei * gi);
+        k->eq[i][1] = k->eq[i][1] + (er * gi + ei * gr);
+    }
+}
+
+/* train_eq, src/equalizer.c:45-58; returns crealf(error) = ref - Re(val) */
+static float train_eq(kal_t *k, const float (*x)[2], float ref) {
+    float vr = 0.0f, vi = 0.0f;
+    for (int i = 0; i < 5; i++) {
+        float a = x[i][0], b = x[i][1], c = k->eq[i][0], d = k->eq[i][1];
+        vr = vr + (a * c - b * d);
+        vi = vi + (a * d + b * c);
+    }
+    float er = ref - vr;   /* conjf(ref - val) = (ref - vr, vi) */
+    float ei = vi;
+    update_eq(k, x, er, ei);
+    return er;
+}
+
+/* data_eq + qpsk_demod, src/equalizer.c:64-90, src/qpsk.c:268-271;
+ * returns the dibit (I<<1)|Q before descrambling */
+static int data_eq(kal_t *k, const float (*x)[2], float soft[2]) {
+    float sr = 0.0f, si = 0.0f;
+    for (int i = 0; i < 5; i++) {
+        float a = x[i][0], b = x[i][1], c = k->eq[i][0], d = -k->eq[i][1];
+        sr = sr + (a * c - b * d);
+        si = si + (a * d + b * c);
+    }
+    int dI = sr < 0.0f;
+    int dQ = si < 0.0f;
+    float cr = dI ? -1.0f : 1.0f;
+    float ci = dQ ? -1.0f : 1.0f;
+    update_eq(k, x, (cr - sr) * 0.1f, (ci - si) * 0.1f);
+    if (soft) {
+        soft[0] = sr;
+        soft[1] = si;
+    }
+    return (dI << 1) | dQ;
+}
+
+int qc_rx_frame(qc_chan_t *ch, const int16_t in[QC_FRAME], uint8_t bits[QC_BITS],
+                qc_trace_t *tr) {
+    const uint32_t n = ch->frame;
+    const int rt = ch->rx_timing;
+    /* M[-48..1190]: m_{n-2}[1832..1879] ++ m_{n-1}[0..1190] (zero before frame 0) */
+    enum { LO = QC_NTAPS - 1, HI = 5 * (QC_DEC - 1) + 255 };
+    float Mbuf[LO + HI + 1][2];
+    float (*M)[2] = Mbuf + LO;
+    for (int t = -LO; t <= HI; t++) {
+        if (t < 0) {
+            if (n >= 2) mix(ch->hist[0], n - 2, QC_FRAME + t, M[t]);
+            else M[t][0] = M[t][1] = 0.0f;
+        } else {
+            if (n >= 1) mix(ch->hist[1], n - 1, t, M[t]);
+            else M[t][0] = M[t][1] = 0.0f;
+        }
+    }
+    /* dec[0..289] (model A) */
+    float dec[QC_DEC + 102][2];
+    memcpy(dec, ch->dprev, sizeof ch->dprev);
+    for (int j = 0; j < 102; j++) fir_at(M + j - LO, dec[QC_DEC + j]);
+    for (int i = 0; i < QC_DEC; i++) fir_at(M + 5 * i + rt - LO, ch->dprev[i]);
+
+    /* preamble hunt, src/qpsk.c:172-183 */
+    float T[255], U[255];
+    for (int j = 0; j < 255; j++) {
+        T[j] = dec[j][0] - dec[j][1];
+        U[j] = dec[j][1] + dec[j][0];
+    }
+    float max_value = 0.0f;
+    int mi = 0;
+    for (int L = 0; L < QC_PRE; L++) {
+        float sr = 0.0f, si = 0.0f;
+        for (int i = 0; i < QC_PRE; i++) {
+            if (k_pre[i] > 0) {
+                sr = sr + T[L + i];
+                si = si + U[L + i];
+            } else {
+                sr = sr - T[L + i];
+                si = si - U[L + i];
+            }
+        }
+        float c = sr * sr + si * si;  /* cnormf, src/qpsk.c:75-80 */
+        if (c > max_value) {
+            max_value = c;
+            mi = L;
+        }
+    }
+
+    /* equalize(), src/qpsk.c:111-123 */
+    kal_t k;
+    kal_reset(&k);
+    int matches = 0;
+    for (int i = 0; i < QC_PRE; i++) {
+        float ref = (float)k_pre[i];
+        if (train_eq(&k, dec + mi + i, ref) * ref > 0.0f) matches++;
+    }
+    const int valid = matches > QC_PRE - 30;  /* src/qpsk.c:196 */
+    memset(bits, 0, QC_BITS);
+    if (tr) memset(tr, 0, sizeof(*tr));
+    if (valid) {
+        const uint8_t *ks = g_ks + (size_t)(((uint64_t)n * 62u) % 32767u);
+        for (int s = 0; s < QC_DSYM; s++) {
+            float soft[2];
+            int dib = data_eq(&k, dec + mi + QC_PRE + s, soft);
+            bits[2 * s] = (uint8_t)((dib & 1) ^ ks[2 * s]);            /* Q */
+            bits[2 * s + 1] = (uint8_t)(((dib >> 1) & 1) ^ ks[2 * s + 1]); /* I */
+            if (tr) {
+                tr->soft[s][0] = soft[0];
+                tr->soft[s][1] = soft[1];
+            }
+        }
+        ch->rx_timing = mi + QC_PRE;  /* src/qpsk.c:219 */
+    }
+    if (tr) {
+        tr->max_index = mi;
+        tr->matches = matches;
+        tr->valid = valid;
+        tr->rx_timing = ch->rx_timing;
+    }
+    memcpy(ch->hist[0], ch->hist[1], sizeof ch->hist[0]);
+    memcpy(ch->hist[1], in, sizeof ch->hist[1]);
+    ch->frame = n + 1;
+    return valid;
+}
+
+typedef struct {
+    const int16_t *in;
+    int nch, nframes, c0, c1;
+    uint8_t *bits, *valid;
+    qc_trace_t *tr;
+    long nvalid;
+} batch_job_t;
+
+static void *batch_worker(void *arg) {
+    batch_job_t *j = (batch_job_t *)arg;
+    qc_chan_t *ch = (qc_chan_t *)malloc(sizeof(qc_chan_t));
+    j->nvalid = 0;
+    for (int c = j->c0; c < j->c1; c++) {
+        qc_chan_init(ch);
+        for (int n = 0; n < j->nframes; n++) {
+            size_t cf = (size_t)c * j->nframes + n;
+            int v = qc_rx_frame(ch, j->in + cf * QC_FRAME, j->bits + cf * QC_BITS,
+                                j->tr ? j->tr + cf : NULL);
+            if (j->valid) j->valid[cf] = (uint8_t)v;
+            j->nvalid += v;
+        }
+    }
+    free(ch);
+    return NULL;
+}
+
+long qc_rx_batch(const int16_t *in, int nch, int nframes, uint8_t *bits,
+                 uint8_t *valid, qc_trace_t *tr, int nthreads) {
+    pthread_once(&g_once, init_tables);
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > nch) nthreads = nch > 0 ? nch : 1;
+    batch_job_t *jobs = (batch_job_t *)calloc((size_t)nthreads, sizeof(batch_job_t));
+    pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
+    for (int t = 0; t < nthreads; t++) {
+        jobs[t] = (batch_job_t){in, nch, nframes, (int)((long)nch * t / nthreads),
+                                (int)((long)nch * (t + 1) / nthreads), bits, valid, tr, 0};
+        if (nthreads > 1) pthread_create(&th[t], NULL, batch_worker, &jobs[t]);
+        else batch_worker(&jobs[t]);
+    }
+    long total = 0;
+    for (int t = 0; t < nthreads; t++) {
+        if (nthreads > 1) pthread_join(th[t], NULL);
+        total += jobs[t].nvalid;
+    }
+    free(jobs);
+    free(th);
+    return total;
+}
+
+/* ------------------------------------------------------------------ TX */
+
+void qc_tx_init(qc_tx_t *tx) {
+    pthread_once(&g_once, init_tables);
+    memset(tx, 0, sizeof(*tx));
+    tx->phase[0] = 1.0f;  /* fbb_tx_phase = cmplx(0.0f), src/qpsk.c:375 */
+}
+
+/* fbb_tx_rect = cmplx(TAU*CENTER/FS), src/qpsk.c:376 (argument rounded to float) */
+static void tx_rect(float r[2]) {
+    const float arg = (float)(2.0f * 3.14159265358979323846 * 1100.0f / 8000.0f);
+    r[0] = cosf(arg);
+    r[1] = sinf(arg);
+}
+
+int qc_tx_frame(qc_tx_t *tx, int16_t *out, const float (*sym)[2], int len,
+                int preamble) {
+    const int n = len * 5;
+    float (*sig)[2] = (float (*)[2])calloc((size_t)n, sizeof(float[2]));
+    for (int i = 0; i < len; i++) {   /* zero-stuff x5, src/qpsk.c:285-291 */
+        sig[5 * i][0] = sym[i][0];
+        sig[5 * i][1] = sym[i][1];
+    }
+    for (int j = 0; j < n; j++) {      /* fir(tx_filter, ...), src/fir.c:29-43 */
+        memmove(tx->fir_mem[0], tx->fir_mem[1], sizeof(float[2]) * (QC_NTAPS - 1));
+        tx->fir_mem[QC_NTAPS - 1][0] = sig[j][0];
+        tx->fir_mem[QC_NTAPS - 1][1] = sig[j][1];
+        fir_at((const float (*)[2])tx->fir_mem, sig[j]);
+    }
+    float r[2];
+    tx_rect(r);
+    for (int i = 0; i < n; i++) {      /* mix up, src/qpsk.c:301-304 */
+        float a = tx->phase[0] * r[0] - tx->phase[1] * r[1];
+        float b = tx->phase[0] * r[1] + tx->phase[1] * r[0];
+        tx->phase[0] = a;
+        tx->phase[1] = b;
+        float sr = sig[i][0] * a - sig[i][1] * b;
+        float si = sig[i][0] * b + sig[i][1] * a;
+        sig[i][0] = sr;
+        sig[i][1] = si;
+    }
+    /* fbb_tx_phase /= cabsf(...), src/qpsk.c:306; glibc hypotf is the
+     * correctly rounded double-evaluated norm */
+    float mag = (float)sqrt((double)tx->phase[0] * tx->phase[0] +
+                            (double)tx->phase[1] * tx->phase[1]);
+    tx->phase[0] = tx->phase[0] / mag;
+    tx->phase[1] = tx->phase[1] / mag;
+    for (int i = 0; i < n; i++)        /* src/qpsk.c:313-319 */
+        out[i] = (int16_t)(sig[i][0] * (preamble ? 8192.0f : 16384.0f));
+    free(sig);
+    return n;
+}
+
+static uint64_t sm64(uint64_t *s) {
+    uint64_t z = (*s += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+/* mean square of noiseless data samples (data RMS ~7,200) */
+#define QC_PDATA 5.19e7
+
+void qc_synth_channel(uint64_t seed, uint32_t c, double ebn0_db, int16_t *out,
+                      long nsamples, uint8_t *unused) {
+    (void)unused;
+    uint64_t s = seed ^ ((uint64_t)c * 0x9E3779B97F4A7C15ull);
+    qc_tx_t tx;
+    qc_tx_init(&tx);
+    long pos = (long)(sm64(&s) % QC_PACKET);  /* leading delay d_c */
+    if (pos > nsamples) pos = nsamples;
+    memset(out, 0, sizeof(int16_t) * (size_t)pos);
+    float pre[QC_PRE][2], dsym[QC_DSYM][2];
+    for (int i = 0; i < QC_PRE; i++) pre[i][0] = pre[i][1] = (float)k_pre[i];
+    int16_t buf[640];
+    while (pos < nsamples) {
+        int m = qc_tx_frame(&tx, buf, (const float (*)[2])pre, QC_PRE, 1);
+        for (int i = 0; i < m && pos < nsamples; i++) out[pos++] = buf[i];
+        for (int f = 0; f < 8; f++) {
+            for (int i = 0; i < QC_DSYM; i++) {  /* qpsk_mod, src/qpsk.c:251-256 */
+                uint64_t dib = sm64(&s) & 3u;
+                dsym[i][0] = (dib >> 1) ? -1.0f : 1.0f;  /* I odd bit  */
+                dsym[i][1] = (dib & 1) ? -1.0f : 1.0f;   /* Q even bit */
+            }
+            m = qc_tx_frame(&tx, buf, (const float (*)[2])dsym, QC_DSYM, 0);
+            for (int i = 0; i < m && pos < nsamples; i++) out[pos++] = buf[i];
+        }
+        for (int i = 0; i < 903 && pos < nsamples; i++) out[pos++] = 0;
+    }
+    if (ebn0_db >= 100.0) return;
+    /* AWGN: sigma^2 = P_data * Fs / (2 * Rb * 10^(EbN0/10)), Rb = 3200 b/s */
+    const double sigma = sqrt(1.25 * QC_PDATA / pow(10.0, ebn0_db / 10.0));
+    for (long t = 0; t < nsamples; t++) {
+        uint64_t k = seed ^ 0x5851F42D4C957F2Dull;
+        k ^= ((uint64_t)c << 32) ^ (uint64_t)t;
+        uint64_t h1 = sm64(&k), h2 = sm64(&k);
+        double u1 = ((double)(h1 >> 11) + 1.0) * 0x1p-53;
+        double u2 = (double)(h2 >> 11) * 0x1p-53;
+        double z = sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
+        double v = nearbyint((double)out[t] + sigma * z);
+        if (v > 32767.0) v = 32767.0;
+        if (v < -32768.0) v = -32768.0;
+        out[t] = (int16_t)v;
+    }
+}
+
+typedef struct {
+    uint64_t seed;
+    uint32_t c0;
+    int lo, hi;
+    double ebn0;
+    int16_t *out;
+    long ns;
+} synth_job_t;
+
+static void *synth_worker(void *arg) {
+    synth_job_t *j = (synth_job_t *)arg;
+    for (int c = j->lo; c < j->hi; c++)
+        qc_synth_channel(j->seed, j->c0 + (uint32_t)c, j->ebn0, j->out + (size_t)c * j->ns,
+                         j->ns, NULL);
+    return NULL;
+}
+
+void qc_synth_batch(uint64_t seed, uint32_t c0, int nch, double ebn0_db,
+                    int16_t *out, long nsamples, int nthreads) {
+    pthread_once(&g_once, init_tables);
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > nch) nthreads = nch > 0 ? nch : 1;
+    synth_job_t *jobs = (synth_job_t *)calloc((size_t)nthreads, sizeof(synth_job_t));
+    pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
+    for (int t = 0; t < nthreads; t++) {
+        jobs[t] = (synth_job_t){seed, c0, (int)((long)nch * t / nthreads),
+                                (int)((long)nch * (t + 1) / nthreads), ebn0_db, out, nsamples};
+        pthread_create(&th[t], NULL, synth_worker, &jobs[t]);
+    }
+    for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+    free(jobs);
+    free(th);
+}

@@ -1,0 +1,90 @@
+"""Generate the golden fixtures in tests/golden/ from the UNMODIFIED reference.
+
+Runs in the build container only (needs /root/reference and oracle/_ref, built
+by `make -C oracle ref`).  Inputs are either the reference's own data file
+(preamble_qpsk_8k.raw, copied here as a data fixture) or synthetic channel
+streams regenerated from a seed by the oracle's TX restatement (the input's
+sha256 is stored so the generator itself is pinned).  Every expected output
+below comes from oracle/_ref/libqpsk_ref.so, i.e. the reference's own code.
+
+    python tests/golden/make_golden.py
+"""
+import hashlib
+import json
+import os
+import shutil
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+import oracle  # noqa: E402
+
+SYNTH_CASES = [  # (name, seed, nch, nframes, ebn0_db)
+    ("synth_s1_clean", 1, 64, 16, 1000.0),
+    ("synth_s2_eb8", 2, 64, 16, 8.0),
+    ("synth_s3_eb4", 3, 64, 16, 4.0),
+    ("synth_s4_eb0", 4, 64, 16, 0.0),
+]
+
+
+def bitstr(b):
+    return "".join(str(int(v)) for v in b)
+
+
+def main():
+    oracle.build(ref=True)
+    assert oracle.ref_available()
+    # 1. the reference's sample capture, through the reference driver semantics
+    src = "/root/reference/preamble_qpsk_8k.raw"
+    dst = os.path.join(HERE, "preamble_qpsk_8k.raw")
+    shutil.copyfile(src, dst)
+    raw = np.fromfile(dst, np.int16)
+    nf = raw.size // oracle.FRAME
+    x = raw[: nf * oracle.FRAME].reshape(1, nf, oracle.FRAME)
+    bits, valid, tr, log = oracle.ref_rx(x, trace=True, log=True)
+    recs = b"".join(np.concatenate([bits[0, n], np.zeros(496 - 62, np.uint8)]).tobytes()
+                    for n in range(nf) if valid[0, n])
+    dec, mixed, _, _ = oracle.ref_stages(x)
+    exp = {
+        "input": "preamble_qpsk_8k.raw",
+        "input_md5": hashlib.md5(raw.tobytes()).hexdigest(),
+        "frames": int(nf),
+        "output_bytes": len(recs),
+        "output_md5": hashlib.md5(recs).hexdigest(),
+        "trace": [{k: int(tr[0, n][k]) for k in ("max_index", "matches", "valid", "rx_timing")}
+                  for n in range(nf)],
+        "valid_bits": {str(n): bitstr(bits[0, n]) for n in range(nf) if valid[0, n]},
+        "debug2": log.splitlines(),
+    }
+    with open(os.path.join(HERE, "sample_expected.json"), "w") as f:
+        json.dump(exp, f, indent=1)
+    np.savez_compressed(os.path.join(HERE, "sample_stages.npz"), dec=dec,
+                        soft=tr[0]["soft"], valid=valid[0])
+
+    # 2. KATs straight from the reference: mixer table and keystream
+    ones = np.full((1, 2, oracle.FRAME), 16384, np.int16)   # x/16384 == 1
+    _, mixed1, _, _ = oracle.ref_stages(ones)
+    nz = 530                                                 # 530*62 > 32767 + 62
+    zb, zv, _ = oracle.ref_rx(np.zeros((1, nz, oracle.FRAME), np.int16))
+    assert zv.all(), "all-zero frames are always valid (matches == 128)"
+    np.savez_compressed(os.path.join(HERE, "kat.npz"), mixer_frame0=mixed1[0],
+                        mixer_frame1=mixed1[1], keystream=zb[0].reshape(-1))
+
+    # 3. seeded synthetic channels (noiseless and AWGN)
+    for name, seed, nch, nfr, eb in SYNTH_CASES:
+        xs = oracle.synth(seed, nch, nfr, eb)
+        b, v, t = oracle.ref_rx(xs, trace=True)
+        soft = np.where(v[..., None, None].astype(bool), t["soft"], 0).astype(np.float32)
+        np.savez_compressed(
+            os.path.join(HERE, name + ".npz"), seed=seed, nch=nch, nframes=nfr, ebn0_db=eb,
+            input_sha256=hashlib.sha256(xs.tobytes()).hexdigest(),
+            bits=np.packbits(b, axis=-1), valid=v, max_index=t["max_index"],
+            matches=t["matches"], rx_timing=t["rx_timing"], soft=soft)
+        print(name, "valid frac %.3f" % v.mean())
+    print("sample:", exp["output_md5"], exp["output_bytes"], "B")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,113 @@
+"""Pin the oracle (clean-room restatement oracle/cpu_ref.c) to the reference.
+
+Goldens in tests/golden/ were produced by the UNMODIFIED reference
+(tests/golden/make_golden.py).  Where oracle/_ref is present the restatement is
+also diffed live against the reference on fresh random channels.
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+
+SYNTH = ["synth_s1_clean", "synth_s2_eb8", "synth_s3_eb4", "synth_s4_eb0"]
+
+
+def _sample(golden_dir):
+    raw = np.fromfile(os.path.join(golden_dir, "preamble_qpsk_8k.raw"), np.int16)
+    nf = raw.size // oracle.FRAME
+    return raw[: nf * oracle.FRAME].reshape(1, nf, oracle.FRAME)
+
+
+def test_sample_file_md5(golden_dir):
+    """C1: the reference's capture through the restatement = reference output
+    (src/qpsk.c:436-458 record format, md5 b56a4d36...)."""
+    exp = json.load(open(os.path.join(golden_dir, "sample_expected.json")))
+    raw = open(os.path.join(golden_dir, "preamble_qpsk_8k.raw"), "rb").read()
+    assert hashlib.md5(raw).hexdigest() == exp["input_md5"] == "1175fea4332f8e742524d49641e32c62"
+    x = _sample(golden_dir)
+    bits, valid, tr = oracle.cpu_rx(x, trace=True)
+    recs = b"".join(np.concatenate([bits[0, n], np.zeros(434, np.uint8)]).tobytes()
+                    for n in range(x.shape[1]) if valid[0, n])
+    assert len(recs) == exp["output_bytes"] == 1984
+    assert hashlib.md5(recs).hexdigest() == exp["output_md5"] == "b56a4d3609d0312934aaef69903c5298"
+    for n, t in enumerate(exp["trace"]):
+        for k in ("max_index", "matches", "valid", "rx_timing"):
+            assert int(tr[0, n][k]) == t[k], (n, k)
+    st = np.load(os.path.join(golden_dir, "sample_stages.npz"))
+    vm = st["valid"].astype(bool)
+    np.testing.assert_array_equal(tr[0]["soft"][vm], st["soft"][vm])
+
+
+def test_mixer_table_kat(golden_dir):
+    """P[t] = R^(t+1) (src/qpsk.c:139) and the (-1)^n frame alternation."""
+    kat = np.load(os.path.join(golden_dir, "kat.npz"))
+    p = oracle.mixer_table()
+    np.testing.assert_array_equal(p, kat["mixer_frame0"])
+    np.testing.assert_array_equal(-p, kat["mixer_frame1"])
+    assert p[0].view(np.uint32).tolist() == [0x3F26423A, 0xBF42A9F7]
+    assert (p == 0).sum() == 93
+
+
+def test_keystream_kat(golden_dir):
+    """Descrambler keystream: frame n uses bits [62n, 62n+62) (src/scramble.c)."""
+    kat = np.load(os.path.join(golden_dir, "kat.npz"))
+    ks = oracle.keystream(kat["keystream"].size)
+    np.testing.assert_array_equal(ks, kat["keystream"])
+    assert "".join(map(str, ks[:62])) == \
+        "00000011111101100000100000110100001100001011100010100011100100"
+    full = oracle.keystream(2 * 32767)
+    np.testing.assert_array_equal(full[:32767], full[32767:])  # maximal-length LFSR
+
+
+@pytest.mark.parametrize("name", SYNTH)
+def test_synth_goldens(golden_dir, name):
+    g = np.load(os.path.join(golden_dir, name + ".npz"))
+    x = oracle.synth(int(g["seed"]), int(g["nch"]), int(g["nframes"]), float(g["ebn0_db"]))
+    assert hashlib.sha256(x.tobytes()).hexdigest() == str(g["input_sha256"])
+    bits, valid, tr = oracle.cpu_rx(x, trace=True)
+    np.testing.assert_array_equal(np.packbits(bits, axis=-1), g["bits"])
+    np.testing.assert_array_equal(valid, g["valid"])
+    for k in ("max_index", "matches", "rx_timing"):
+        np.testing.assert_array_equal(tr[k], g[k])
+    vm = valid.astype(bool)
+    np.testing.assert_array_equal(tr["soft"][vm], g["soft"][vm])
+
+
+def test_edge_inputs_vs_reference():
+    """Saturated, alternating and all-zero frames: restatement == reference."""
+    if not oracle.ref_available():
+        pytest.skip("oracle/_ref not built (no /root/reference here)")
+    rng = np.random.default_rng(5)
+    x = np.stack([
+        np.zeros((6, oracle.FRAME), np.int16),
+        np.full((6, oracle.FRAME), 32767, np.int16),
+        np.full((6, oracle.FRAME), -32768, np.int16),
+        np.tile(np.array([32767, -32768], np.int16), (6, oracle.FRAME // 2)),
+        rng.integers(-32768, 32768, (6, oracle.FRAME)).astype(np.int16),
+        rng.integers(-3, 4, (6, oracle.FRAME)).astype(np.int16),
+    ])
+    b1, v1, t1 = oracle.cpu_rx(x, trace=True)
+    b2, v2, t2 = oracle.ref_rx(x, trace=True)
+    np.testing.assert_array_equal(v1, v2)
+    np.testing.assert_array_equal(b1, b2)
+    for k in ("max_index", "matches", "rx_timing"):
+        np.testing.assert_array_equal(t1[k], t2[k])
+
+
+@pytest.mark.parametrize("ebn0", [1000.0, 6.0, 2.0])
+def test_random_channels_vs_reference(ebn0):
+    if not oracle.ref_available():
+        pytest.skip("oracle/_ref not built (no /root/reference here)")
+    x = oracle.synth(1234 + int(ebn0), 48, 20, ebn0, c0=1000)
+    b1, v1, t1 = oracle.cpu_rx(x, trace=True)
+    b2, v2, t2 = oracle.ref_rx(x, trace=True)
+    np.testing.assert_array_equal(v1, v2)
+    np.testing.assert_array_equal(b1, b2)
+    for k in ("max_index", "matches", "rx_timing"):
+        np.testing.assert_array_equal(t1[k], t2[k])
+    vm = v2.astype(bool)
+    np.testing.assert_array_equal(t1["soft"][vm], t2["soft"][vm])
