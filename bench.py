@@ -1,0 +1,200 @@
+#!/usr/bin/env python3
+"""bench.py -- demodulated Msamples/s of the MI355X QPSK receive path.
+
+One "step" = demodulating one batch: every channel of the workload advances by
+`--frames` 1880-sample frames (C3: 65536 channels x 32 frames = 3.94e9 int16
+samples, 7.88 GB, resident in HBM before timing).  Channels are independent,
+so N GPUs each take their own 65536-channel shard (distinct channels, no
+collective; "scaling": "weak"; --strong splits one 65536-channel batch).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+Rank 0 prints ONE JSON line.  See DESIGN.md "Measurement" for every field.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "demodulated Msamples/sec (whole node), 65536-channel 8 kHz batch; BER vs ref"
+FRAME = 1880
+ALG_BYTES_PER_FRAME = 3760 + 63     # int16 in + 62 bit-bytes + valid byte
+HBM_PEAK_GBS = 8000.0               # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+VALU_PEAK_TOPS = 78.6               # fp32 non-FMA lane-ops/s: 256 CU x 128 lanes x 2.4 GHz
+OPS_PER_SAMPLE_MIN = 96.0           # minimal bit-exact formulation
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--channels", type=int, default=65536, help="channels per GPU (weak)")
+    ap.add_argument("--frames", type=int, default=32)
+    ap.add_argument("--ebn0", type=float, default=1000.0, help=">= 100: noiseless")
+    ap.add_argument("--seed", type=int, default=3)
+    ap.add_argument("--strong", action="store_true", help="split --channels across ranks")
+    ap.add_argument("--cpu-channels", type=int, default=2048,
+                    help="channels of the bounded CPU-baseline sample (0: skip)")
+    ap.add_argument("--verify", type=int, default=256,
+                    help="channels checked against the oracle after timing (0: skip)")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import singlecarrier_amd as sc
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    if args.strong:
+        base, rem = divmod(args.channels, world)
+        nch = base + (1 if rank < rem else 0)
+        c0 = rank * base + min(rank, rem)
+    else:
+        nch, c0 = args.channels, rank * args.channels
+    nf = args.frames
+
+    t = time.perf_counter()
+    x_host = sc.synth(args.seed, nch, nf, args.ebn0, c0=c0, threads=16)
+    t_synth = time.perf_counter() - t
+    t = time.perf_counter()
+    x = torch.from_numpy(x_host).to(f"cuda:{local}")
+    torch.cuda.synchronize()
+    t_h2d = time.perf_counter() - t
+    bits = torch.empty((nch, nf, 62), dtype=torch.uint8, device=x.device)
+    valid = torch.empty((nch, nf), dtype=torch.uint8, device=x.device)
+    rx = sc.Receiver(nch, device=local)
+
+    for _ in range(args.warmup):
+        rx.demod_device(x, bits, valid)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    rx.timing(True)
+    rx.collect_timing()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record()
+    for _ in range(args.steps):
+        rx.demod_device(x, bits, valid)
+    ev1.record()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    if dist:
+        dist.barrier()
+    kern_ms, launches = rx.collect_timing()
+    rx.timing(False)
+    region_ms = ev0.elapsed_time(ev1)
+
+    tmax = wall
+    if dist:
+        tt = torch.tensor([wall], dtype=torch.float64, device=x.device)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        tmax = float(tt.item())
+        ntot = torch.tensor([nch], dtype=torch.float64, device=x.device)
+        dist.all_reduce(ntot)
+        total_ch = int(ntot.item())
+    else:
+        total_ch = nch
+    samples = float(total_ch) * nf * FRAME * args.steps
+    value = samples / tmax / 1e6
+
+    # per-launch roofline of the dominant kernel (rx_step_kernel, one per frame)
+    t_launch = kern_ms / 1e3 / max(launches, 1)
+    achieved = nch * ALG_BYTES_PER_FRAME / t_launch / 1e9
+    roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                "kernel": "rx_step_kernel", "launch_us": round(t_launch * 1e6, 2),
+                "alg_bytes_per_launch": nch * ALG_BYTES_PER_FRAME}
+    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc):
+        p = json.load(open(pmc))
+        if p.get("channels") == nch:
+            roofline["traffic"] = p["hbm_bytes_per_launch"]
+            roofline["traffic_source"] = p.get("source")
+    per_gpu_sps = nch * FRAME / t_launch
+    valu = {"ops_per_sample": OPS_PER_SAMPLE_MIN,
+            "achieved_Tops": round(per_gpu_sps * OPS_PER_SAMPLE_MIN / 1e12, 2),
+            "peak_Tops": VALU_PEAK_TOPS,
+            "frac": round(per_gpu_sps * OPS_PER_SAMPLE_MIN / 1e12 / VALU_PEAK_TOPS, 4)}
+
+    # parity spot check of the timed outputs (checker only; not timed)
+    verified = None
+    if args.verify and rank == 0:
+        import oracle
+        k = min(args.verify, nch)
+        # the timed context advanced (warmup + steps) batches of the same
+        # input: the oracle replays that whole stream for the first k channels
+        reps = args.warmup + args.steps
+        exp_bits, exp_valid, _ = oracle.cpu_rx(np.concatenate([x_host[:k]] * reps, axis=1))
+        verified = bool((bits[:k].cpu().numpy() == exp_bits[:, -nf:]).all()
+                        and (valid[:k].cpu().numpy() == exp_valid[:, -nf:]).all())
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_channels > 0:
+        import oracle
+        k = min(args.cpu_channels, nch)
+        sample = x_host[:k]
+        if oracle.ref_available():
+            t = time.perf_counter()
+            oracle.ref_rx(sample)
+            dt = time.perf_counter() - t
+            cpu = {"value": round(k * nf * FRAME / dt / 1e6, 3), "unit": "Msamples/s",
+                   "cores": 1, "kind": "reference",
+                   "sample": f"{k} of the {nch} channels x {nf} frames, unmodified reference "
+                             f"(oracle/_ref, gcc -O2), one channel after another, {dt:.1f} s"}
+        else:
+            t = time.perf_counter()
+            oracle.cpu_rx(sample, threads=1)
+            dt = time.perf_counter() - t
+            cpu = {"value": round(k * nf * FRAME / dt / 1e6, 3), "unit": "Msamples/s",
+                   "cores": 1, "kind": "port",
+                   "sample": f"{k} channels x {nf} frames, oracle/cpu_ref.c, 1 thread, {dt:.1f} s"}
+
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": round(value, 3), "unit": "Msamples/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(tmax / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "strong" if args.strong else "weak", "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic: reference TX packets, splitmix64 dibits, per-channel delay"
+                    + ("" if args.ebn0 >= 100 else f", AWGN Eb/N0 {args.ebn0} dB"),
+            "config": {"workload": f"{nch} channels x {nf} frames x 1880 samples per GPU "
+                                   f"(C3{'/C4' if world > 1 else ''})",
+                       "channels_per_gpu": nch, "channels_total": total_ch, "frames": nf,
+                       "samples_per_step": int(total_ch * nf * FRAME),
+                       "parallelism": f"channel shards x{world}, no collective"},
+            "roofline": roofline, "valu": valu, "cpu_baseline": cpu,
+            "region_ms_per_step": round(region_ms / args.steps, 3),
+            "synth_s": round(t_synth, 2), "h2d_s": round(t_h2d, 2),
+            "h2d_incl_msamples_s": round(nch * nf * FRAME / (t_h2d + tmax / args.steps) / 1e6, 1),
+            "verified_vs_oracle": verified,
+        }
+        print(json.dumps(out), flush=True)
+    rx.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

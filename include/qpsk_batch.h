@@ -1,0 +1,83 @@
+/*
+ * qpsk_batch.h -- batched, multi-channel C-ABI of the MI355X receive path.
+ *
+ * Replaces the reference's single-channel driver loop (src/qpsk.c:436-458,
+ * which calls qpsk_rx_frame() once per 1880-sample frame, src/qpsk.c:447)
+ * with one call over many independent channels.  Each channel behaves exactly
+ * like a fresh run of the reference receiver fed that channel's stream; the
+ * per-channel state the reference keeps in statics (src/qpsk.c:37-53,
+ * src/kalman.c:19-35, src/scramble.c:41-42) lives in the context and persists
+ * across calls, so a stream may be fed in any number of calls.
+ *
+ * Layouts (row-major, little endian):
+ *   in     int16  [nch][nframes][1880]   raw 8 kHz samples (reference .raw framing)
+ *   bits   uint8  [nch][nframes][62]     0/1 per bit, reference order
+ *                                         (bits[2s] = Q, bits[2s+1] = I, descrambled);
+ *                                         all zero for invalid frames
+ *   valid  uint8  [nch][nframes]         qpsk_rx_frame() return value
+ *   trace  int32  [nch][nframes][4]      optional: max_index, matches, valid,
+ *                                         rx_timing after the frame
+ *   soft   float  [nch][nframes][31][2]  optional: data_eq soft symbols (valid
+ *                                         frames; zero otherwise)
+ * Any optional pointer may be NULL.
+ *
+ * Errors: functions return 0 on success or a negative QPSK_E* code; HIP errors
+ * are QPSK_EHIP - (int)hipError_t.  Contexts are independent and may be used
+ * from different host threads; one context must not be used concurrently.
+ */
+#pragma once
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct qpsk_ctx qpsk_ctx;
+
+enum {
+    QPSK_OK = 0,
+    QPSK_EINVAL = -1,     /* bad argument (NULL ctx/in, nch < 1, nframes < 0) */
+    QPSK_ENOMEM = -2,     /* device or host allocation failed */
+    QPSK_ENODEV = -3,     /* no such HIP device */
+    QPSK_EHIP = -1000,    /* QPSK_EHIP - hipError_t */
+};
+
+/* Create a receiver for nch channels on HIP device `device`, in the reference's
+ * initial RX state (src/qpsk.c:427-434).  Returns NULL on failure; *err (if
+ * non-NULL) receives the error code. */
+qpsk_ctx *qpsk_rx_create(int device, int nch, int *err);
+void qpsk_rx_destroy(qpsk_ctx *ctx);
+/* Back to the initial state (all channels), as after qpsk_rx_create. */
+int qpsk_rx_reset(qpsk_ctx *ctx);
+int qpsk_rx_channels(const qpsk_ctx *ctx);
+/* Frames received so far by every channel of the context. */
+uint64_t qpsk_rx_frames(const qpsk_ctx *ctx);
+
+/* Host-memory call: copies `in` to the device, demodulates nframes frames of
+ * every channel, copies the results back and synchronises. */
+int qpsk_rx_batch(qpsk_ctx *ctx, const int16_t *in, int nframes, uint8_t *bits,
+                  uint8_t *valid, int32_t *trace, float *soft);
+
+/* Device-memory call: all pointers are device pointers on the context's device;
+ * the work is enqueued on `stream` (a hipStream_t, NULL = default stream) and
+ * the call returns without synchronising.  Launches one fused kernel per frame
+ * plus one history update. */
+int qpsk_rx_batch_device(qpsk_ctx *ctx, const int16_t *d_in, int nframes,
+                         uint8_t *d_bits, uint8_t *d_valid, int32_t *d_trace,
+                         float *d_soft, void *stream);
+
+/* Kernel-time accounting.  When enabled, every qpsk_rx_batch_device call
+ * records a HIP event pair on its stream around its step-kernel launches (one
+ * per frame); collect() waits for them and returns the summed span (ms) and the
+ * number of step launches since the previous collect. */
+int qpsk_rx_timing_enable(qpsk_ctx *ctx, int on);
+int qpsk_rx_timing_collect(qpsk_ctx *ctx, float *ms, int *launches);
+
+/* Message for an error code (static storage). */
+const char *qpsk_strerror(int err);
+
+#ifdef __cplusplus
+}
+#endif

@@ -151,6 +151,33 @@ def ref_stages(x):
     return dec, mixed, bits, valid
 
 
+def _tx_packets(init, frame, symbols):
+    outs = []
+    init()
+    for sym, pre in symbols:
+        s = np.ascontiguousarray(np.asarray(sym, np.complex64)).view(np.float32)
+        out = np.zeros(5 * (s.size // 2), np.int16)
+        n = frame(_p(out), _p(s), s.size // 2, int(pre))
+        outs.append(out[:n])
+    return outs
+
+
+def cpu_tx(symbols):
+    """TX restatement: symbols = [(complex array, is_preamble), ...] -> [int16 arrays]."""
+    lib = cpu_lib()
+    lib.qc_tx_frame.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int]
+    st = C.create_string_buffer(49 * 8 + 8)
+    return _tx_packets(lambda: lib.qc_tx_init(st),
+                       lambda o, s, n, p: lib.qc_tx_frame(st, o, s, n, p), symbols)
+
+
+def ref_tx(symbols):
+    """The unmodified reference transmitter qpsk_tx_frame (src/qpsk.c:278)."""
+    lib = ref_lib()
+    lib.ref_tx_frame.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int]
+    return _tx_packets(lib.ref_tx_reset, lib.ref_tx_frame, symbols)
+
+
 def synth(seed: int, nch: int, nframes: int, ebn0_db: float = 1000.0, c0: int = 0,
           threads: int = 0) -> np.ndarray:
     """Synthetic channel streams [nch][nframes][1880] int16."""

@@ -44,6 +44,10 @@ int ref_rx_batch(const int16_t *in, int nch, int nframes, uint8_t *bits,
 void ref_peek_dec(float out[290][2]);
 void ref_peek_mixed(float out[1880][2]);
 
+/* Reference TX (src/qpsk.c:278-322) after main()'s TX setup; sym re/im pairs. */
+void ref_tx_reset(void);
+int ref_tx_frame(int16_t *out, const float *sym, int len, int preamble);
+
 /* Byte distance between decimated_frame and input_frame in this build. */
 long ref_layout_gap(void);
 

@@ -109,3 +109,21 @@ void ref_peek_mixed(float out[FRAME_SIZE][2]) {  /* input_frame[1880..3759] */
         out[i][1] = cimagf(input_frame[FRAME_SIZE + i]);
     }
 }
+
+/* Reference transmitter (src/qpsk.c:278-322) with main()'s TX setup
+ * (src/qpsk.c:361-365, 375-376); sym is interleaved re/im. */
+void ref_tx_reset(void) {
+    memset(tx_filter, 0, sizeof tx_filter);
+    for (size_t i = 0; i < PREAMBLE_LENGTH; i++) {
+        float val = (float)preamblevalues[i];
+        preambletable[i] = val + (val * I);
+    }
+    fbb_tx_phase = cmplx(0.0f);
+    fbb_tx_rect = cmplx(TAU * CENTER / FS);
+}
+
+int ref_tx_frame(int16_t *out, const float *sym, int len, int preamble) {
+    complex float s[len];
+    for (int i = 0; i < len; i++) s[i] = sym[2 * i] + sym[2 * i + 1] * I;
+    return qpsk_tx_frame(out, s, len, preamble != 0);
+}

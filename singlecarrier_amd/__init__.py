@@ -1,0 +1,262 @@
+"""singlecarrier_amd -- MI355X receive path of the SingleCarrier QPSK modem.
+
+Python mirror of the C-ABI in ``include/qpsk_internal.h`` (the reference's
+``headers/qpsk_internal.h:79-84`` surface) and ``include/qpsk_batch.h`` (the
+batched, multi-channel receiver), over ``singlecarrier_amd/libqpsk_hip.so``.
+
+There is no CPU fallback: if the HIP library is missing or no GPU is present,
+the receive functions raise.  (The CPU restatement in ``oracle/`` is test
+infrastructure, never called from here.)
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libqpsk_hip.so")
+
+FRAME_SIZE = 1880        # headers/qpsk_internal.h:45
+DATA_SYMBOLS = 31        # headers/qpsk_internal.h:37
+PREAMBLE_LENGTH = 128    # headers/qpsk_internal.h:50
+BITS_PER_FRAME = 496     # headers/qpsk_internal.h:48 (record size of the RX driver)
+NBITS = 62               # bits written per valid frame (src/qpsk.c:206-215)
+CYCLES = 5
+
+_lib = None
+
+
+class _CF(C.Structure):
+    _fields_ = [("re", C.c_float), ("im", C.c_float)]
+
+
+class QpskError(RuntimeError):
+    pass
+
+
+def build(verbose: bool = False) -> str:
+    """Compile libqpsk_hip.so for gfx950 (hipcc cross-compiles without a GPU)."""
+    out = subprocess.run(["make", "-C", os.path.join(HERE, "csrc")], capture_output=True,
+                         text=True)
+    if out.returncode != 0:
+        raise QpskError("build failed:\n" + out.stdout[-4000:] + out.stderr[-4000:])
+    if verbose:
+        print(out.stdout)
+    return LIB_PATH
+
+
+def lib():
+    """Load the HIP library (fails loudly when it is missing)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise QpskError(f"{LIB_PATH} not built: run singlecarrier_amd.build() "
+                            "or make -C singlecarrier_amd/csrc")
+        try:  # share torch's HIP runtime when torch is in use (same soname)
+            import torch  # noqa: F401
+        except Exception:
+            pass
+        L = C.CDLL(LIB_PATH)
+        vp, i32, u64 = C.c_void_p, C.c_int, C.c_uint64
+        L.qpsk_rx_create.restype = vp
+        L.qpsk_rx_create.argtypes = [i32, i32, C.POINTER(C.c_int)]
+        L.qpsk_rx_destroy.argtypes = [vp]
+        L.qpsk_rx_reset.argtypes = [vp]
+        L.qpsk_rx_channels.argtypes = [vp]
+        L.qpsk_rx_frames.restype = u64
+        L.qpsk_rx_frames.argtypes = [vp]
+        L.qpsk_rx_batch.argtypes = [vp, vp, i32, vp, vp, vp, vp]
+        L.qpsk_rx_batch_device.argtypes = [vp, vp, i32, vp, vp, vp, vp, vp]
+        L.qpsk_strerror.restype = C.c_char_p
+        L.qpsk_strerror.argtypes = [i32]
+        L.qpsk_rx_frame.argtypes = [vp, vp]
+        L.qpsk_tx_frame.argtypes = [vp, vp, i32, C.c_bool]
+        L.qpsk_surface_error.restype = i32
+        L.qpsk_rx_timing_enable.argtypes = [vp, i32]
+        L.qpsk_rx_timing_collect.argtypes = [vp, C.POINTER(C.c_float), C.POINTER(C.c_int)]
+        L.qpsk_synth_batch.restype = None
+        L.qpsk_synth_batch.argtypes = [u64, C.c_uint32, i32, C.c_double, vp, C.c_long, i32]
+        L.cnormf.restype = C.c_float
+        L.cnormf.argtypes = [_CF]   # _Complex float == {float, float} in one SSE reg (SysV)
+        _lib = L
+    return _lib
+
+
+SYMBOLS = ["qpsk_rx_create", "qpsk_rx_destroy", "qpsk_rx_reset", "qpsk_rx_channels",
+           "qpsk_rx_frames", "qpsk_rx_batch", "qpsk_rx_batch_device", "qpsk_strerror",
+           "cnormf", "qpsk_mod", "qpsk_demod", "qpsk_rx_frame", "qpsk_tx_frame",
+           "qpsk_rx_init", "qpsk_tx_init", "qpsk_surface_error", "qpsk_tx_state_init",
+           "qpsk_tx_frame_state", "qpsk_synth_batch", "qpsk_rx_timing_enable",
+           "qpsk_rx_timing_collect"]
+
+
+def _check(rc: int) -> None:
+    if rc != 0:
+        raise QpskError(f"qpsk error {rc}: {lib().qpsk_strerror(rc).decode()}")
+
+
+def _ptr(a) -> int | None:
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data
+    return a.data_ptr()  # torch tensor (device memory)
+
+
+class Receiver:
+    """A batch of ``nch`` independent receivers on one GPU (``qpsk_ctx``).
+
+    Each channel behaves like the reference receiver fed that channel's stream
+    from a fresh start (src/qpsk.c:427-458); state persists across calls.
+    """
+
+    def __init__(self, nch: int, device: int = 0):
+        err = C.c_int(0)
+        self._h = lib().qpsk_rx_create(device, nch, C.byref(err))
+        if not self._h:
+            _check(err.value or -3)
+        self.nch = nch
+        self.device = device
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            lib().qpsk_rx_destroy(self._h)
+            self._h = None
+
+    __del__ = close
+
+    def reset(self) -> None:
+        _check(lib().qpsk_rx_reset(self._h))
+
+    @property
+    def frames(self) -> int:
+        return int(lib().qpsk_rx_frames(self._h))
+
+    def timing(self, on: bool = True) -> None:
+        """Enable per-call step-kernel span events (see qpsk_rx_timing_collect)."""
+        _check(lib().qpsk_rx_timing_enable(self._h, int(on)))
+
+    def collect_timing(self):
+        """(summed step-kernel span in ms, number of step launches) since last collect."""
+        ms, n = C.c_float(0), C.c_int(0)
+        _check(lib().qpsk_rx_timing_collect(self._h, C.byref(ms), C.byref(n)))
+        return float(ms.value), int(n.value)
+
+    def demod(self, x, trace: bool = False, soft: bool = False):
+        """Host arrays: x int16 [nch][nframes][1880] -> dict of numpy arrays
+        bits [nch][nframes][62], valid [nch][nframes] (+ trace [..][4], soft [..][31][2])."""
+        x = np.ascontiguousarray(x, dtype=np.int16)
+        if x.ndim != 3 or x.shape[0] != self.nch or x.shape[2] != FRAME_SIZE:
+            raise ValueError(f"expected int16 [{self.nch}][nframes][{FRAME_SIZE}], got {x.shape}")
+        nf = x.shape[1]
+        out = {"bits": np.zeros((self.nch, nf, NBITS), np.uint8),
+               "valid": np.zeros((self.nch, nf), np.uint8)}
+        if trace:
+            out["trace"] = np.zeros((self.nch, nf, 4), np.int32)
+        if soft:
+            out["soft"] = np.zeros((self.nch, nf, DATA_SYMBOLS, 2), np.float32)
+        _check(lib().qpsk_rx_batch(self._h, _ptr(x), nf, _ptr(out["bits"]), _ptr(out["valid"]),
+                                   _ptr(out.get("trace")), _ptr(out.get("soft"))))
+        return out
+
+    def demod_device(self, x, bits, valid, trace=None, soft=None, stream=None) -> None:
+        """Device tensors (torch, on this device): enqueue on ``stream``
+        (default: torch's current stream) and return without synchronising."""
+        import torch
+        if x.dtype != torch.int16 or x.dim() != 3 or x.shape[0] != self.nch \
+                or x.shape[2] != FRAME_SIZE or not x.is_contiguous() or not x.is_cuda:
+            raise ValueError("x must be a contiguous cuda int16 [nch][nframes][1880] tensor")
+        nf = x.shape[1]
+        for name, t, shape in (("bits", bits, (self.nch, nf, NBITS)),
+                               ("valid", valid, (self.nch, nf)),
+                               ("trace", trace, (self.nch, nf, 4)),
+                               ("soft", soft, (self.nch, nf, DATA_SYMBOLS, 2))):
+            if t is not None and (tuple(t.shape) != shape or not t.is_contiguous() or not t.is_cuda):
+                raise ValueError(f"{name} must be a contiguous cuda tensor of shape {shape}")
+        if stream is None:
+            stream = torch.cuda.current_stream(x.device)
+        _check(lib().qpsk_rx_batch_device(self._h, _ptr(x), nf, _ptr(bits), _ptr(valid),
+                                          _ptr(trace), _ptr(soft), C.c_void_p(stream.cuda_stream)))
+
+
+# --- the reference's single-channel surface (headers/qpsk_internal.h:79-84) ---
+
+def cnormf(val: complex) -> float:
+    """|val|^2 as the reference computes it (src/qpsk.c:75-80)."""
+    return float(lib().cnormf(_CF(val.real, val.imag)))
+
+
+def qpsk_mod(bits, index: int) -> complex:
+    """Gray map: I = bits[index+1], Q = bits[index] (src/qpsk.c:251-256)."""
+    i = -1.0 if bits[index + 1] == 1 else 1.0
+    q = -1.0 if bits[index] == 1 else 1.0
+    return complex(i, q)
+
+
+def qpsk_demod(symbol: complex) -> list:
+    """[Q, I] hard decisions, bits[1] = Re<0, bits[0] = Im<0 (src/qpsk.c:268-271)."""
+    return [int(np.float32(symbol.imag) < 0), int(np.float32(symbol.real) < 0)]
+
+
+def qpsk_rx_init() -> None:
+    lib().qpsk_rx_init()
+    _check(lib().qpsk_surface_error())
+
+
+def qpsk_rx_frame(frame, bits=None):
+    """One 1880-sample frame through the one-channel GPU receiver (src/qpsk.c:133).
+    Returns 1 and fills bits[0..61] on a valid frame, else 0."""
+    fr = np.ascontiguousarray(frame, dtype=np.int16)
+    if fr.shape != (FRAME_SIZE,):
+        raise ValueError("frame must be 1880 int16 samples")
+    b = np.zeros(NBITS, np.uint8)
+    v = lib().qpsk_rx_frame(_ptr(fr), _ptr(b))
+    _check(lib().qpsk_surface_error())
+    if v and bits is not None:
+        bits[:NBITS] = b
+    return v, b
+
+
+def qpsk_tx_init() -> None:
+    lib().qpsk_tx_init()
+
+
+def qpsk_tx_frame(symbols, preamble: bool) -> np.ndarray:
+    """Host TX of the reference (src/qpsk.c:278-322): len(symbols) complex
+    symbols -> 5*len int16 samples."""
+    s = np.ascontiguousarray(np.asarray(symbols, np.complex64))
+    out = np.zeros(s.size * CYCLES, np.int16)
+    n = lib().qpsk_tx_frame(_ptr(out), _ptr(s), s.size, bool(preamble))
+    return out[:n]
+
+
+def synth(seed: int, nch: int, nframes: int, ebn0_db: float = 1000.0, c0: int = 0,
+          threads: int = 0) -> np.ndarray:
+    """Synthetic channel streams int16 [nch][nframes][1880] (include/qpsk_synth.h)."""
+    out = np.empty((nch, nframes, FRAME_SIZE), np.int16)
+    threads = threads or min(16, os.cpu_count() or 1)
+    lib().qpsk_synth_batch(seed, c0, nch, float(ebn0_db), _ptr(out), nframes * FRAME_SIZE,
+                           threads)
+    return out
+
+
+def read_raw(path: str) -> np.ndarray:
+    """A reference .raw capture as frames [nframes][1880]; the short tail is
+    dropped like the reference driver (src/qpsk.c:442-445)."""
+    raw = np.fromfile(path, np.int16)
+    nf = raw.size // FRAME_SIZE
+    return raw[: nf * FRAME_SIZE].reshape(nf, FRAME_SIZE)
+
+
+def records(bits: np.ndarray, valid: np.ndarray) -> bytes:
+    """The reference driver's output file (src/qpsk.c:455-457): one 496-byte
+    record per valid frame, bits in bytes 0..61, the rest zero."""
+    out = bytearray()
+    for n in np.flatnonzero(valid):
+        rec = np.zeros(BITS_PER_FRAME, np.uint8)
+        rec[:NBITS] = bits[n]
+        out += rec.tobytes()
+    return bytes(out)

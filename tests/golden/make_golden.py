@@ -29,6 +29,15 @@ SYNTH_CASES = [  # (name, seed, nch, nframes, ebn0_db)
 ]
 
 
+# src/constants.c:25-42
+PREAMBLE = [-1, 1, 1, -1, -1, 1, 1, 1, -1, 1, -1, -1, 1, 1, -1, -1, 1, 1, -1, 1, -1, -1, 1, -1,
+            1, -1, 1, -1, 1, -1, 1, 1, 1, -1, 1, 1, 1, 1, -1, -1, 1, -1, -1, 1, 1, -1, 1, -1,
+            1, 1, -1, 1, -1, -1, 1, -1, -1, -1, -1, 1, 1, -1, 1, -1, 1, 1, 1, -1, -1, 1, 1, -1,
+            1, 1, -1, -1, 1, 1, -1, 1, 1, -1, 1, 1, -1, -1, -1, 1, -1, 1, -1, 1, -1, -1, -1, 1,
+            -1, -1, 1, -1, 1, 1, -1, -1, -1, -1, -1, 1, 1, 1, -1, 1, 1, -1, 1, 1, -1, -1, 1, 1,
+            -1, 1, -1, 1, -1, -1, -1, 1]
+
+
 def bitstr(b):
     return "".join(str(int(v)) for v in b)
 
@@ -83,6 +92,21 @@ def main():
             bits=np.packbits(b, axis=-1), valid=v, max_index=t["max_index"],
             matches=t["matches"], rx_timing=t["rx_timing"], soft=soft)
         print(name, "valid frac %.3f" % v.mean())
+    # 4. reference transmitter (src/qpsk.c:278-342): 3 packets, seeded dibits
+    pre = np.array([complex(p, p) for p in PREAMBLE], np.complex64)
+    rng = np.random.default_rng(42)
+    syms = []
+    for _ in range(3):
+        syms.append((pre, True))
+        for _ in range(8):
+            d = rng.integers(0, 4, 31)
+            syms.append((np.array([complex(-1 if v >> 1 else 1, -1 if v & 1 else 1) for v in d],
+                                  np.complex64), False))
+    out = oracle.ref_tx(syms)
+    np.savez_compressed(os.path.join(HERE, "tx_golden.npz"),
+                        symbols=np.concatenate([s for s, _ in syms]),
+                        preamble=np.array([p for _, p in syms]),
+                        lengths=np.array([len(s) for s, _ in syms]), samples=np.concatenate(out))
     print("sample:", exp["output_md5"], exp["output_bytes"], "B")
 
 

@@ -1,0 +1,185 @@
+"""Parity of the MI355X receive path with the reference (run with -m gpu).
+
+Every comparison is exact: bits, valid flags, max_index/matches/rx_timing
+traces and the soft I/Q symbols of valid frames are compared bit for bit
+(the north_star's 1e-5 RMS soft-symbol tolerance is therefore
+met with zero error).  Expected values come from the golden fixtures made by
+the unmodified reference (tests/golden/make_golden.py) and, at larger sizes,
+from the oracle restatement (oracle/cpu_ref.c), itself pinned to the reference
+by tests/test_oracle.py.
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+import singlecarrier_amd as sc
+
+pytestmark = pytest.mark.gpu
+
+SYNTH = ["synth_s1_clean", "synth_s2_eb8", "synth_s3_eb4", "synth_s4_eb0"]
+
+
+def _sample(golden_dir):
+    return sc.read_raw(os.path.join(golden_dir, "preamble_qpsk_8k.raw"))
+
+
+def _assert_same(out, bits, valid, tr):
+    np.testing.assert_array_equal(out["valid"], valid)
+    np.testing.assert_array_equal(out["bits"], bits)
+    if tr is not None and "trace" in out:
+        t = out["trace"]
+        np.testing.assert_array_equal(t[..., 0], tr["max_index"])
+        np.testing.assert_array_equal(t[..., 1], tr["matches"])
+        np.testing.assert_array_equal(t[..., 2], tr["valid"])
+        np.testing.assert_array_equal(t[..., 3], tr["rx_timing"])
+    if tr is not None and "soft" in out:
+        vm = valid.astype(bool)
+        np.testing.assert_array_equal(out["soft"][vm], tr["soft"][vm])
+        assert not out["soft"][~vm].any()
+
+
+def _vs_oracle(x, **kw):
+    rx = sc.Receiver(x.shape[0])
+    out = rx.demod(x, trace=True, soft=True)
+    bits, valid, tr = oracle.cpu_rx(x, trace=True)
+    _assert_same(out, bits, valid, tr)
+    rx.close()
+    return out
+
+
+def test_sample_file_md5(golden_dir):
+    """C1 config: preamble_qpsk_8k.raw -> reference output file md5."""
+    exp = json.load(open(os.path.join(golden_dir, "sample_expected.json")))
+    frames = _sample(golden_dir)
+    rx = sc.Receiver(1)
+    out = rx.demod(frames[None], trace=True, soft=True)
+    recs = sc.records(out["bits"][0], out["valid"][0])
+    assert hashlib.md5(recs).hexdigest() == exp["output_md5"] == "b56a4d3609d0312934aaef69903c5298"
+    for n, t in enumerate(exp["trace"]):
+        assert list(out["trace"][0, n]) == [t["max_index"], t["matches"], t["valid"], t["rx_timing"]]
+    st = np.load(os.path.join(golden_dir, "sample_stages.npz"))
+    vm = st["valid"].astype(bool)
+    np.testing.assert_array_equal(out["soft"][0][vm], st["soft"][vm])
+
+
+def test_reference_surface_rx_frame(golden_dir):
+    """qpsk_rx_frame() drop-in (headers/qpsk_internal.h:83) frame by frame."""
+    exp = json.load(open(os.path.join(golden_dir, "sample_expected.json")))
+    sc.qpsk_rx_init()
+    recs = b""
+    for fr in _sample(golden_dir):
+        v, b = sc.qpsk_rx_frame(fr)
+        if v:
+            recs += np.concatenate([b, np.zeros(434, np.uint8)]).tobytes()
+    assert hashlib.md5(recs).hexdigest() == exp["output_md5"]
+
+
+@pytest.mark.parametrize("name", SYNTH)
+def test_synth_goldens(golden_dir, name):
+    g = np.load(os.path.join(golden_dir, name + ".npz"))
+    x = oracle.synth(int(g["seed"]), int(g["nch"]), int(g["nframes"]), float(g["ebn0_db"]))
+    assert hashlib.sha256(x.tobytes()).hexdigest() == str(g["input_sha256"])
+    rx = sc.Receiver(x.shape[0])
+    out = rx.demod(x, trace=True, soft=True)
+    np.testing.assert_array_equal(np.packbits(out["bits"], axis=-1), g["bits"])
+    np.testing.assert_array_equal(out["valid"], g["valid"])
+    np.testing.assert_array_equal(out["trace"][..., 0], g["max_index"])
+    np.testing.assert_array_equal(out["trace"][..., 1], g["matches"])
+    np.testing.assert_array_equal(out["trace"][..., 3], g["rx_timing"])
+    np.testing.assert_array_equal(out["soft"], g["soft"])
+
+
+def test_c2_4096_channels():
+    """C2 config: 4096 synthetic channels x 16 frames, bit-exact."""
+    x = oracle.synth(1, 4096, 16)
+    out = _vs_oracle(x)
+    assert 0.2 < out["valid"].mean() < 0.7
+
+
+@pytest.mark.parametrize("nch", [1, 2, 63, 65, 130])
+def test_ragged_channel_counts(nch):
+    x = oracle.synth(77 + nch, nch, 12, 5.0)
+    _vs_oracle(x)
+
+
+def test_edge_inputs():
+    rng = np.random.default_rng(5)
+    x = np.stack([
+        np.zeros((8, 1880), np.int16),
+        np.full((8, 1880), 32767, np.int16),
+        np.full((8, 1880), -32768, np.int16),
+        np.tile(np.array([32767, -32768], np.int16), (8, 940)),
+        rng.integers(-32768, 32768, (8, 1880)).astype(np.int16),
+        rng.integers(-3, 4, (8, 1880)).astype(np.int16),
+    ])
+    _vs_oracle(x)
+
+
+def test_streaming_split_equals_one_call():
+    """State (rx_timing, carried symbols, sample history, frame counter) persists
+    across calls: feeding 16 frames as 5+1+1+9 == one 16-frame call."""
+    x = oracle.synth(9, 192, 16, 6.0)
+    rx1 = sc.Receiver(192)
+    whole = rx1.demod(x, trace=True, soft=True)
+    rx2 = sc.Receiver(192)
+    parts = [rx2.demod(np.ascontiguousarray(x[:, a:b]), trace=True, soft=True)
+             for a, b in ((0, 5), (5, 6), (6, 7), (7, 16))]
+    assert rx2.frames == 16
+    for k in ("bits", "valid", "trace", "soft"):
+        np.testing.assert_array_equal(np.concatenate([p[k] for p in parts], axis=1), whole[k])
+    rx2.reset()
+    again = rx2.demod(x, trace=True, soft=True)
+    np.testing.assert_array_equal(again["bits"], whole["bits"])
+
+
+def test_independent_contexts():
+    xa = oracle.synth(21, 70, 8)
+    xb = oracle.synth(22, 70, 8, 4.0)
+    ra, rb = sc.Receiver(70), sc.Receiver(70)
+    oa1 = ra.demod(xa[:, :4])
+    ob = rb.demod(xb)
+    oa2 = ra.demod(np.ascontiguousarray(xa[:, 4:]))
+    bits, valid, _ = oracle.cpu_rx(xa)
+    np.testing.assert_array_equal(np.concatenate([oa1["bits"], oa2["bits"]], 1), bits)
+    np.testing.assert_array_equal(ob["bits"], oracle.cpu_rx(xb)[0])
+
+
+def test_device_api_torch():
+    import torch
+    x = oracle.synth(31, 256, 10, 7.0)
+    bits, valid, tr = oracle.cpu_rx(x, trace=True)
+    rx = sc.Receiver(256)
+    dx = torch.from_numpy(x).cuda()
+    db = torch.zeros((256, 10, 62), dtype=torch.uint8, device="cuda")
+    dv = torch.zeros((256, 10), dtype=torch.uint8, device="cuda")
+    dt = torch.zeros((256, 10, 4), dtype=torch.int32, device="cuda")
+    ds = torch.zeros((256, 10, 31, 2), dtype=torch.float32, device="cuda")
+    rx.demod_device(dx, db, dv, dt, ds)
+    torch.cuda.synchronize()
+    _assert_same({"bits": db.cpu().numpy(), "valid": dv.cpu().numpy(),
+                  "trace": dt.cpu().numpy(), "soft": ds.cpu().numpy()}, bits, valid, tr)
+
+
+@pytest.mark.parametrize("ebn0", [0.0, 3.0, 6.0, 10.0])
+def test_awgn_sweep_points(ebn0):
+    """C5 config points (reduced channel count): zero disagreement vs reference."""
+    x = oracle.synth(500 + int(ebn0), 1024, 16, ebn0)
+    _vs_oracle(x)
+
+
+def test_full_size_c3():
+    """C3 config at full size (65536 channels x 32 frames): every channel's
+    bits, valid flags and rx_timing trace equal the oracle's."""
+    nch, nf = 65536, 32
+    x = oracle.synth(3, nch, nf)
+    rx = sc.Receiver(nch)
+    out = rx.demod(x, trace=True)
+    bits, valid, tr = oracle.cpu_rx(x, trace=True)
+    np.testing.assert_array_equal(out["valid"], valid)
+    np.testing.assert_array_equal(out["bits"], bits)
+    np.testing.assert_array_equal(out["trace"][..., 3], tr["rx_timing"])
+    np.testing.assert_array_equal(out["trace"][..., 0], tr["max_index"])
