@@ -101,7 +101,7 @@ def main():
     wall = time.perf_counter() - t0
     if dist:
         dist.barrier()
-    kern_ms, launches = rx.collect_timing()
+    kern_ms, kern_frames = rx.collect_timing()
     rx.timing(False)
     region_ms = ev0.elapsed_time(ev1)
 
@@ -118,20 +118,22 @@ def main():
     samples = float(total_ch) * nf * FRAME * args.steps
     value = samples / tmax / 1e6
 
-    # per-launch roofline of the dominant kernel (rx_step_kernel, one per frame)
-    t_launch = kern_ms / 1e3 / max(launches, 1)
-    achieved = nch * ALG_BYTES_PER_FRAME / t_launch / 1e9
+    # roofline of the dominant kernel (rx_kernel: one persistent launch per step,
+    # all `frames` frames of all channels); duration from HIP events on its stream
+    t_launch = kern_ms / 1e3 / args.steps
+    alg_bytes = nch * nf * ALG_BYTES_PER_FRAME
+    achieved = alg_bytes / t_launch / 1e9
     roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-                "kernel": "rx_step_kernel", "launch_us": round(t_launch * 1e6, 2),
-                "alg_bytes_per_launch": nch * ALG_BYTES_PER_FRAME}
+                "kernel": "rx_kernel", "launch_us": round(t_launch * 1e6, 2),
+                "alg_bytes_per_launch": alg_bytes}
     pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc):
         p = json.load(open(pmc))
-        if p.get("channels") == nch:
+        if p.get("channels") == nch and p.get("frames") == nf:
             roofline["traffic"] = p["hbm_bytes_per_launch"]
             roofline["traffic_source"] = p.get("source")
-    per_gpu_sps = nch * FRAME / t_launch
+    per_gpu_sps = nch * nf * FRAME / t_launch
     valu = {"ops_per_sample": OPS_PER_SAMPLE_MIN,
             "achieved_Tops": round(per_gpu_sps * OPS_PER_SAMPLE_MIN / 1e12, 2),
             "peak_Tops": VALU_PEAK_TOPS,

@@ -1,0 +1,81 @@
+"""Summarise a profiles/profile.sh run: per-kernel average duration and
+per-dispatch PMC averages for rx_step_kernel, HBM traffic per launch with the
+gfx950 FETCH_SIZE correction (MI355X_MICROARCH.md 'HBM': FETCH_SIZE counts
+half the bytes of wide coalesced reads -> x2), writes profiles/<tag>_summary.md
+and profiles/pmc_traffic.json.
+
+    python profiles/summarize.py gpurun_out/prof_v1 TAG CHANNELS FRAMES [KERNEL]
+"""
+import csv
+import glob
+import json
+import os
+import re
+import sys
+from collections import defaultdict
+
+d, tag, nch, nfr = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4])
+K = sys.argv[5] if len(sys.argv) > 5 else "rx_kernel"
+
+
+def rows(pattern):
+    out = []
+    for f in glob.glob(os.path.join(d, pattern), recursive=True):
+        out += list(csv.DictReader(open(f)))
+    return out
+
+
+def stats(name):
+    r = rows(f"{name}/**/*kernel_stats.csv")
+    return {short(x["Name"]): (int(x["Calls"]), float(x["AverageNs"])) for x in r}
+
+
+def short(name):
+    m = re.search(r"(\w+)\(", name.replace("(anonymous namespace)", "anon"))
+    return m.group(1) if m else name
+
+
+def counters(name):
+    acc = defaultdict(list)
+    for x in rows(f"{name}/**/*counter_collection.csv"):
+        if K in x["Kernel_Name"]:
+            acc[x["Counter_Name"]].append(float(x["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in acc.items()}
+
+
+lines = [f"# rocprofv3 summary: {tag} ({nch} channels x {nfr} frames per launch)", ""]
+st = stats("stats")
+lines += ["## Kernel durations (kernel-trace --stats)", "",
+          "| kernel | calls | avg us |", "|---|---|---|"]
+for k, (c, a) in sorted(st.items(), key=lambda t: -t[1][0] * t[1][1]):
+    lines.append(f"| {k} | {c} | {a / 1e3:.1f} |")
+for ab in ("abl_back", "abl_front"):
+    s = stats(ab)
+    if K in s:
+        lines.append(f"| {K} [{ab}: only the {ab[4:]} role runs] | {s[K][0]} | {s[K][1] / 1e3:.1f} |")
+c = {}
+for p in ("fetch", "write", "sq", "lds"):
+    c.update(counters(p))
+t_ns = st[K][1]
+fetch_b = c.get("FETCH_SIZE", 0) * 1024 * 2   # KB, x2 gfx950 correction
+write_b = c.get("WRITE_SIZE", 0) * 1024
+alg = nch * nfr * 3823
+lines += ["", f"## Counters per {K} dispatch (averages)", "", "| counter | value |", "|---|---|"]
+for k in sorted(c):
+    lines.append(f"| {k} | {c[k]:.4g} |")
+lines += ["", "## Derived", "",
+          f"- HBM read bytes/launch (2 x FETCH_SIZE): {fetch_b / 1e6:.1f} MB; written (WRITE_SIZE): {write_b / 1e6:.1f} MB",
+          f"- algorithmic bytes/launch: {alg / 1e6:.1f} MB (3823 B per channel-frame, {nch} x {nfr})",
+          f"- traffic / algorithmic = {(fetch_b + write_b) / alg:.2f}",
+          f"- achieved algorithmic GB/s = {alg / t_ns:.1f}; physical GB/s = {(fetch_b + write_b) / t_ns:.1f}"]
+if "SQ_WAVE_CYCLES" in c and "SQ_BUSY_CYCLES" in c:
+    lines.append(f"- VALU instructions per wave-cycle: {c['SQ_INSTS_VALU'] / max(c['SQ_WAVE_CYCLES'], 1):.3f}; "
+                 f"SQ_ACTIVE_INST_VALU/SQ_WAVE_CYCLES = {c['SQ_ACTIVE_INST_VALU'] / c['SQ_WAVE_CYCLES']:.3f}")
+if "GRBM_GUI_ACTIVE" in c:
+    lines.append(f"- effective clock ~ GRBM_GUI_ACTIVE/8/t = {c['GRBM_GUI_ACTIVE'] / 8 / t_ns:.2f} GHz")
+open(os.path.join("profiles", f"{tag}_summary.md"), "w").write("\n".join(lines) + "\n")
+json.dump({"channels": nch, "frames": nfr, "hbm_bytes_per_launch": int(fetch_b + write_b),
+           "fetch_bytes": int(fetch_b), "write_bytes": int(write_b),
+           "source": f"profiles/{tag}_summary.md (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes)"},
+          open(os.path.join("profiles", "pmc_traffic.json"), "w"), indent=1)
+print("\n".join(lines))

@@ -10,14 +10,16 @@
 // reference's order with no contraction (-ffp-contract=off + the pragma below),
 // divisions are correctly rounded, denormals are kept.
 //
-// Per frame the work splits at the preamble decision (DESIGN.md "Kernels"):
-//   front  (wave per channel, LDS-staged):  mixer -> RRC FIR (only the ~290
-//          observable outputs) -> decimation -> 128-lag preamble correlation
-//          -> argmax -> equalizer window dec[mi .. mi+162] to HBM.
-//   back   (lane per channel):  128 train_eq + 31 data_eq steps of the
-//          square-root Kalman equalizer, slicer, descrambler.
-// The front of frame n+1 needs only rx_timing of frame n, so one launch runs
-// front(n+1) and back(n) side by side; both are roles of one kernel.
+// One persistent workgroup of two waves owns a group of 64 channels for every
+// frame of a call (DESIGN.md "Kernels"):
+//   front wave (channel after channel, LDS-staged): mixer -> RRC FIR (only the
+//        290 observable outputs) -> decimation -> 128-lag preamble correlation
+//        -> argmax -> equalizer window dec[mi .. mi+162] -> HBM (L2)
+//   back wave (lane per channel): 128 train_eq + 31 data_eq steps of the
+//        square-root Kalman equalizer, slicer, descrambler.
+// The front of frame n+1 needs only rx_timing of frame n, so in iteration n the
+// front wave works on frame n+1 while the back wave finishes frame n; one
+// __syncthreads() per frame hands rx_timing (LDS) and the window (global) over.
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
@@ -31,13 +33,24 @@
 
 namespace {
 
-constexpr int kBlock = 256;            // 4 waves
-constexpr int kWaves = kBlock / 64;
-constexpr int kChPerWave = QK_GROUP / kWaves;   // front: 16 channels per wave
-// front LDS per wave (float2 units): M1 = m_{n-2}[1832..1879] ++ m_{n-1}[0..1191],
-// M2 = m_{n-1}[1832..1879] ++ m_n[0..103], dec[0..289], TU[0..255]
-constexpr int kM1 = 48 + 1192, kM2 = 48 + 104, kDec = 296, kTU = 256;
-constexpr int kLdsWave = kM1 + kM2 + kDec + kTU;
+// A workgroup owns kGroups groups of 64 channels: waves 0..kGroups-1 are their
+// back waves, waves kGroups.. are front waves, kFrontPer per group.
+constexpr int kGroups = 4;
+constexpr int kFrontPer = 2;
+constexpr int kFrontCh = QK_GROUP / kFrontPer;     // 32 channels per front wave
+constexpr int kFrontWaves = kGroups * kFrontPer;
+constexpr int kBlock = 64 * (kGroups + kFrontWaves);   // 768 threads, 12 waves
+constexpr int kWinStride = 168;        // window row: slot k+1 = dec[mi+k], 84 float4
+// front LDS (float2 units): M = m_{n-2}[1832..1879] ++ m_{n-1}[0..1191]   (1240)
+//                            ++ m_{n-1}[1832..1879] ++ m_n[0..103]        (152)
+// TU (255 correlator terms, permuted) reuses M once the FIR is done.
+constexpr int kM1 = 1240, kM = 1392, kDec = 296;
+constexpr int kItems = kM / 2;         // 696 two-sample (dword) input items
+
+// (re, im) pairs as 2-wide vectors: a complex add / complex*real product is one
+// packed fp32 instruction (v_pk_add_f32 / v_pk_mul_f32: IEEE per lane, no
+// fusion), and the halves never need repacking.
+typedef float f2 __attribute__((ext_vector_type(2)));
 
 constexpr unsigned long long pre_mask(int half) {
     unsigned long long m = 0;
@@ -47,326 +60,527 @@ constexpr unsigned long long pre_mask(int half) {
 }
 constexpr unsigned long long kPreLo = pre_mask(0), kPreHi = pre_mask(1);
 
-struct StepArgs {
+struct RxArgs {
     const int16_t* in;       // [nch][F][1880]
-    const int16_t* hist;     // [nch][2][1880]: frames -2, -1 of this call
+    int16_t* hist;           // [nch][2][1880]: frames -2, -1 of this call
     const float2* ptab;      // [1880] mixer table P[t] * 2^-14
-    const float2* win_rd;    // [ngroup][163][64] equalizer window of frame n
-    float2* win_wr;          // ... of frame n+1
-    const int* mi_rd;
-    int* mi_wr;
-    const int* rt_rd;
-    int* rt_wr;
+    const unsigned long long* ks;  // [1057] keystream bits of frame g (mod 1057)
+    float2* win0;            // [nslot][168] equalizer windows, even global frames
+    float2* win1;            //                                odd global frames
+    int* mi0;                // [nslot] preamble position (even / odd frames)
+    int* mi1;
+    int* rt0;                // [nslot] rx_timing (even / odd frames)
+    int* rt1;
     uint8_t* bits;           // [nch][F][62]
     uint8_t* valid;          // [nch][F]
     int32_t* trace;          // [nch][F][4] or null
     float2* soft;            // [nch][F][31] or null
-    unsigned long long ks;   // keystream bits 62g .. 62g+61 of frame g
-    int nch, F, n, nb_back;
-    unsigned g;              // global frame index of frame n
+    int nch, F;
+    unsigned g0;             // global index of the call's first frame
+    int roles;               // bit 0: back, bit 1: front (3 in production); bits 4-5:
+                             // issue priority boost (0 none, 1 front, 2 back)
 };
 
-__device__ __forceinline__ const int16_t* frame_ptr(const StepArgs& a, int ch, int k) {
+__device__ __forceinline__ float2* win_of(const RxArgs& a, unsigned g) { return (g & 1u) ? a.win1 : a.win0; }
+__device__ __forceinline__ int* mi_of(const RxArgs& a, unsigned g) { return (g & 1u) ? a.mi1 : a.mi0; }
+__device__ __forceinline__ int* rt_of(const RxArgs& a, unsigned g) { return (g & 1u) ? a.rt1 : a.rt0; }
+
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ const int16_t* frame_ptr(const RxArgs& a, int ch, int k) {
     return k >= 0 ? a.in + ((size_t)ch * a.F + k) * QK_FRAME
                   : a.hist + ((size_t)ch * 2 + (k + 2)) * QK_FRAME;
 }
 
-// 8 samples of one frame -> mixed cf32 (src/qpsk.c:139-144 as (-1)^G P[t] x 2^-14)
-__device__ __forceinline__ void mix8(const int16_t* x, int t0, bool neg, const float2* ptab,
-                                     float2* dst) {
-    const int4 raw = *reinterpret_cast<const int4*>(x + t0);
-    const int w[4] = {raw.x, raw.y, raw.z, raw.w};
-#pragma unroll
-    for (int e = 0; e < 8; e++) {
-        const float v = (float)(int16_t)((e & 1) ? (w[e >> 1] >> 16) : (w[e >> 1] & 0xffff));
-        float2 p = ptab[t0 + e];
-        if (neg) { p.x = -p.x; p.y = -p.y; }
-        dst[e] = make_float2(p.x * v, p.y * v);
-    }
+// ---------------------------------------------------------------- front wave
+// Input of one channel for frame n: 696 two-sample items d, item d -> M[2d..2d+1]:
+//   d <  24 : x_{n-2}[1832 + 2d]          d < 620 : x_{n-1}[2(d-24)]
+//   d < 644 : x_{n-1}[1832 + 2(d-620)]    d < 696 : x_n[2(d-644)]
+// Lane l owns items l + 64i, i < 11; i is a compile-time constant below.
+constexpr int kPf = (kItems + 63) / 64;   // 11 prefetched dwords per lane
+
+struct Src {
+    const int16_t* xm2;
+    const int16_t* xm1;
+    const int16_t* x0;
+};
+
+__device__ __forceinline__ Src srcs(const RxArgs& a, int ch, int n) {
+    return {frame_ptr(a, ch, n - 2), frame_ptr(a, ch, n - 1), frame_ptr(a, ch, n)};
 }
 
-// one RRC output, src/fir.c:36-42 (M points at the sample under tap 0)
-__device__ __forceinline__ float2 fir_at(const float2* M) {
-    float yr = 0.0f, yi = 0.0f;
-#pragma unroll
-    for (int k = 0; k < QK_NTAPS; k++) {
-        const float2 m = M[k];
-        yr = yr + m.x * QK_RRC[k];
-        yi = yi + m.y * QK_RRC[k];
+// which frame (0: x_{n-2}, 1: x_{n-1}, 2: x_n; -1: none) and sample index of item l + 64i
+template <int i>
+__device__ __forceinline__ int item(int lane, int& t) {
+    const int d = lane + 64 * i;
+    if (i == 0) {
+        if (lane < 24) { t = 1832 + 2 * lane; return 0; }
+        t = 2 * (lane - 24);
+        return 1;
     }
-    return make_float2(yr * QK_GAIN, yi * QK_GAIN);
+    if (i < 9) { t = 2 * (d - 24); return 1; }
+    if (i == 9) { t = d < 620 ? 2 * (d - 24) : 1832 + 2 * (d - 620); return 1; }
+    if (d < 644) { t = 1832 + 2 * (d - 620); return 1; }
+    if (d < kItems) { t = 2 * (d - 644); return 2; }
+    t = 0;
+    return -1;
 }
 
-// ---------------------------------------------------------------- front role
-__device__ void front_group(const StepArgs& a, int grp, float2* lds) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    float2* M1 = lds + w * kLdsWave;
-    float2* M2 = M1 + kM1;
-    float2* dec = M2 + kM2;
-    float2* TU = dec + kDec;
-    const int n = a.n;
-    const bool neg_m1 = ((a.g - 1u) & 1u) != 0;   // frame g-1
-    const bool neg_02 = (a.g & 1u) != 0;          // frames g and g-2
+template <int i>
+__device__ __forceinline__ void load_item(const Src& s, int lane, int& r) {
+    int t;
+    const int f = item<i>(lane, t);
+    if (f >= 0) r = *reinterpret_cast<const int*>((f == 0 ? s.xm2 : f == 1 ? s.xm1 : s.x0) + t);
+}
 
-    for (int c = 0; c < kChPerWave; c++) {
-        const int col = w * kChPerWave + c;
-        const int ch = grp * QK_GROUP + col;
-        const bool live = ch < a.nch;
-        if (live) {
-            // 1. load + mix: 149 + 6 + 13 + 6 eight-sample items
-            const int16_t* xm1 = frame_ptr(a, ch, n - 1);
-            const int16_t* xm2 = frame_ptr(a, ch, n - 2);
-            const int16_t* x0 = frame_ptr(a, ch, n);
-            for (int it = lane; it < 174; it += 64) {
-                if (it < 149) mix8(xm1, 8 * it, neg_m1, a.ptab, M1 + 48 + 8 * it);
-                else if (it < 155) mix8(xm2, 1832 + 8 * (it - 149), neg_02, a.ptab, M1 + 8 * (it - 149));
-                else if (it < 168) mix8(x0, 8 * (it - 155), neg_02, a.ptab, M2 + 48 + 8 * (it - 155));
-                else mix8(xm1, 1832 + 8 * (it - 168), neg_m1, a.ptab, M2 + 8 * (it - 168));
-            }
-        }
-        __syncthreads();
-        if (live) {
-            // 2. FIR: D_n[i] = fir_out[5i + rt] (decimation, model A) and
-            //    F_{n+1}[j] = fir_out'[j], j < 102 -> dec_{n+1} = [D_n, F_{n+1}]
-            const int rt = a.rt_rd[ch];
-            for (int o = lane; o < QK_NDECOBS; o += 64) {
-                const float2* base = o < QK_NDEC ? M1 + 5 * o + rt : M2 + (o - QK_NDEC);
-                dec[o] = fir_at(base);
-            }
-        }
-        __syncthreads();
-        if (live) {
-            // 3. p*(dr-di, di+dr) == preambletable[i]*dec (p = +-1, exact)
-            for (int j = lane; j < 255; j += 64) {
-                const float2 d = dec[j];
-                TU[j] = make_float2(d.x - d.y, d.y + d.x);
-            }
-        }
-        __syncthreads();
-        if (live) {
-            // 4. correlate lags 2*lane and 2*lane+1, terms in index order
-            float r0 = 0.0f, i0 = 0.0f, r1 = 0.0f, i1 = 0.0f;
-            const float2* tu = TU + 2 * lane;
+__device__ __forceinline__ void prefetch(const Src& s, int lane, int (&r)[kPf]) {
+    load_item<0>(s, lane, r[0]); load_item<1>(s, lane, r[1]); load_item<2>(s, lane, r[2]);
+    load_item<3>(s, lane, r[3]); load_item<4>(s, lane, r[4]); load_item<5>(s, lane, r[5]);
+    load_item<6>(s, lane, r[6]); load_item<7>(s, lane, r[7]); load_item<8>(s, lane, r[8]);
+    load_item<9>(s, lane, r[9]); load_item<10>(s, lane, r[10]);
+}
+
+// src/qpsk.c:139-144 as (-1)^G * P[t] * (x * 2^-14), two samples per item
+template <int i>
+__device__ __forceinline__ void mix_item(int lane, int r, bool neg_odd, bool neg_even,
+                                         const float2* P, float2* M) {
+    int t;
+    const int f = item<i>(lane, t);
+    if (f < 0) return;
+    const float4 p = *reinterpret_cast<const float4*>(P + t);
+    const float sg = (f == 1 ? neg_odd : neg_even) ? -1.0f : 1.0f;   // exact sign flip
+    const float v0 = (float)(int16_t)(r & 0xffff);
+    const float v1 = (float)(int16_t)(r >> 16);
+    *reinterpret_cast<float4*>(M + 2 * (lane + 64 * i)) =
+        make_float4((sg * p.x) * v0, (sg * p.y) * v0, (sg * p.z) * v1, (sg * p.w) * v1);
+}
+
+__device__ __forceinline__ void mix(int lane, const int (&r)[kPf], unsigned g, const float2* P,
+                                    float2* M) {
+    const bool no = ((g - 1u) & 1u) != 0, ne = (g & 1u) != 0;   // frames g-1 | g, g-2
+    mix_item<0>(lane, r[0], no, ne, P, M); mix_item<1>(lane, r[1], no, ne, P, M);
+    mix_item<2>(lane, r[2], no, ne, P, M); mix_item<3>(lane, r[3], no, ne, P, M);
+    mix_item<4>(lane, r[4], no, ne, P, M); mix_item<5>(lane, r[5], no, ne, P, M);
+    mix_item<6>(lane, r[6], no, ne, P, M); mix_item<7>(lane, r[7], no, ne, P, M);
+    mix_item<8>(lane, r[8], no, ne, P, M); mix_item<9>(lane, r[9], no, ne, P, M);
+    mix_item<10>(lane, r[10], no, ne, P, M);
+}
+
+// max over the 64 lanes of a wave (DPP row shifts / row broadcasts, no LDS trips)
+__device__ __forceinline__ unsigned wave_max_u32(unsigned v) {
+    v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false)); // row_shr:1
+    v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false)); // row_shr:2
+    v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xe, false)); // row_shr:4
+    v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xc, false)); // row_shr:8
+    v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false)); // row_bcast:15
+    v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false)); // row_bcast:31
+    return (unsigned)__builtin_amdgcn_readlane((int)v, 63);
+}
+
+__device__ __forceinline__ f2 ld2(const float2* p) { return *reinterpret_cast<const f2*>(p); }
+
+// One channel of frame n's front: D_n (decimated with rx_timing rt), F_{n+1},
+// correlation of dec_{n+1} = [D_n, F_{n+1}] and its argmax mi.
+__device__ __forceinline__ int front_channel(int lane, int rt, float2* M, float2* dec) {
+    // RRC (src/fir.c:36-42), outputs accumulated in tap order.  Decimated
+    // outputs D[o] = fir_out[5o + rt] (model A): lane l makes
+    // o = 3l..3l+2 from the 59 samples M[15l + rt + s], read in batches.
+    if (lane < 63) {
+        const float2* b = M + 15 * lane + rt;
+        f2 y[3] = {{0.0f, 0.0f}, {0.0f, 0.0f}, {0.0f, 0.0f}};
 #pragma unroll
-            for (int s = 0; s <= QK_NPRE; s++) {
-                const float2 v = tu[s];
-                if (s < QK_NPRE) {
-                    if (QK_PRE[s] > 0) { r0 = r0 + v.x; i0 = i0 + v.y; }
-                    else { r0 = r0 - v.x; i0 = i0 - v.y; }
-                }
-                if (s >= 1) {
-                    if (QK_PRE[s - 1] > 0) { r1 = r1 + v.x; i1 = i1 + v.y; }
-                    else { r1 = r1 - v.x; i1 = i1 - v.y; }
-                }
-            }
-            float c0 = r0 * r0 + i0 * i0;          // cnormf, src/qpsk.c:75-80
-            float c1 = r1 * r1 + i1 * i1;
-            // 5. first strict maximum over lags (src/qpsk.c:176-183); NaN never wins
-            c0 = (c0 == c0) ? c0 : -1.0f;
-            c1 = (c1 == c1) ? c1 : -1.0f;
-            float best = c0;
-            int idx = 2 * lane;
-            if (c1 > best) { best = c1; idx = 2 * lane + 1; }
+        for (int s0 = 0; s0 < 59; s0 += 15) {
+            f2 v[15];
 #pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {
-                const float ob = __shfl_xor(best, off);
-                const int oi = __shfl_xor(idx, off);
-                if (ob > best || (ob == best && oi < idx)) { best = ob; idx = oi; }
+            for (int j = 0; j < 15; j++)
+                if (s0 + j < 59) v[j] = ld2(b + s0 + j);
+#pragma unroll
+            for (int j = 0; j < 15; j++) {
+                const int s = s0 + j;
+#pragma unroll
+                for (int m = 0; m < 3; m++) {
+                    const int k = s - 5 * m;
+                    if (s < 59 && k >= 0 && k < QK_NTAPS) y[m] = y[m] + v[j] * QK_RRC[k];
+                }
             }
-            const int mi = best > 0.0f ? idx : 0;
-            // 6. equalizer window of frame n+1, layout [grp][k][64 channels]
-            float2* wo = a.win_wr + (size_t)grp * QK_NWIN * QK_GROUP + col;
-            for (int k = lane; k < QK_NWIN; k += 64) wo[(size_t)k * QK_GROUP] = dec[mi + k];
-            if (lane == 0) a.mi_wr[ch] = mi;
         }
-        __syncthreads();
+#pragma unroll
+        for (int m = 0; m < 3; m++)
+            if (3 * lane + m < QK_NDEC) {
+                const f2 o = y[m] * QK_GAIN;
+                dec[3 * lane + m] = make_float2(o.x, o.y);
+            }
+    }
+    // Undecimated head F_{n+1}[j] = fir_out'[j], j < 102: lane l makes j = 2l, 2l+1
+    if (lane < 51) {
+        const float2* b = M + kM1 + 2 * lane;
+        f2 y[2] = {{0.0f, 0.0f}, {0.0f, 0.0f}};
+#pragma unroll
+        for (int s0 = 0; s0 < 50; s0 += 10) {
+            f2 v[10];
+#pragma unroll
+            for (int j = 0; j < 10; j++) v[j] = ld2(b + s0 + j);
+#pragma unroll
+            for (int j = 0; j < 10; j++) {
+                const int s = s0 + j;
+#pragma unroll
+                for (int m = 0; m < 2; m++) {
+                    const int k = s - m;
+                    if (k >= 0 && k < QK_NTAPS) y[m] = y[m] + v[j] * QK_RRC[k];
+                }
+            }
+        }
+#pragma unroll
+        for (int m = 0; m < 2; m++) {
+            const f2 o = y[m] * QK_GAIN;
+            dec[QK_NDEC + 2 * lane + m] = make_float2(o.x, o.y);
+        }
+    }
+    wave_lds_sync();
+    // p*(dr-di, di+dr) == preambletable[i]*dec[j] exactly (p = +-1); TU reuses M,
+    // even j first so that lane l's term s is at a lane-contiguous position.
+    float2* TU = M;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const int j = lane + 64 * r;
+        if (j < 255) {
+            const float2 d = dec[j];
+            TU[(j & 1) ? 128 + (j >> 1) : (j >> 1)] = make_float2(d.x - d.y, d.y + d.x);
+        }
+    }
+    wave_lds_sync();
+    // correlate lags 2*lane and 2*lane+1 (src/qpsk.c:88-96), terms in index
+    // order; acc = acc +- (T, U) is one packed add
+    f2 acc0 = {0.0f, 0.0f}, acc1 = {0.0f, 0.0f};
+#pragma unroll
+    for (int s0 = 0; s0 <= QK_NPRE; s0 += 16) {
+        f2 v[16];
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+            const int s = s0 + j;
+            if (s <= QK_NPRE) v[j] = ld2(TU + ((s & 1) ? 128 + lane + (s >> 1) : lane + (s >> 1)));
+        }
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+            const int s = s0 + j;
+            if (s < QK_NPRE) acc0 = QK_PRE[s] > 0 ? acc0 + v[j] : acc0 - v[j];
+            if (s >= 1 && s <= QK_NPRE) acc1 = QK_PRE[s - 1] > 0 ? acc1 + v[j] : acc1 - v[j];
+        }
+    }
+    const float r0 = acc0.x, i0 = acc0.y, r1 = acc1.x, i1 = acc1.y;
+    const float c0 = r0 * r0 + i0 * i0;    // cnormf, src/qpsk.c:75-80
+    const float c1 = r1 * r1 + i1 * i1;
+    // hunt (src/qpsk.c:172-183): first lag whose value is > the running max,
+    // which starts at 0.  Values are >= 0 or NaN (never selected): map to
+    // non-negative float bits (monotone as unsigned), take the wave max, then the
+    // lowest lag holding it; a maximum of 0 leaves max_index at 0.
+    const unsigned k0 = c0 > 0.0f ? __float_as_uint(c0) : 0u;
+    const unsigned k1 = c1 > 0.0f ? __float_as_uint(c1) : 0u;
+    const unsigned km = wave_max_u32(max(k0, k1));
+    if (km == 0u) return 0;
+    const unsigned long long m0 = __ballot(k0 == km), m1 = __ballot(k1 == km);
+    const int i0x = m0 ? 2 * (__ffsll((long long)m0) - 1) : 1 << 20;
+    const int i1x = m1 ? 2 * (__ffsll((long long)m1) - 1) + 1 : 1 << 20;
+    return min(i0x, i1x);
+}
+
+// window slots (2q, 2q+1) = dec[mi+2q-1], dec[mi+2q] (slot 0 unused); 84
+// float4 = 1344 B per channel, full 128-B lines
+__device__ __forceinline__ void store_window(int lane, int mi, const float2* dec, float2* out) {
+    float4* o = reinterpret_cast<float4*>(out);
+    {
+        const float2 lo = dec[max(mi + 2 * lane - 1, 0)], hi = dec[mi + 2 * lane];
+        o[lane] = make_float4(lo.x, lo.y, hi.x, hi.y);
+    }
+    if (lane < kWinStride / 2 - 64) {
+        const int q = lane + 64;
+        const float2 lo = dec[mi + 2 * q - 1], hi = dec[mi + 2 * q];
+        o[q] = make_float4(lo.x, lo.y, hi.x, hi.y);
     }
 }
 
 // ---------------------------------------------------------------- back role
+// Complex values are f2 = (re, im).  cmul(A, C) = (ac - bd, ad + bc) with every
+// product and the final sum/difference rounded once, exactly as gcc expands
+// the reference's complex products for finite operands: two packed multiplies
+// and one packed add (neg on the low half), no fusion.
+// (a.x - b.x, a.y + b.y) as ONE v_pk_add_f32 with the low half of b negated
+// (LLVM builds it from two packed adds plus moves otherwise); a + (-b) == a - b.
+__device__ __forceinline__ f2 addsub(f2 a, f2 b) {
+    f2 r;
+    asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ f2 cmul(f2 A, f2 C) {
+    const f2 t1 = A.xx * C;       // (ac, ad)
+    const f2 t2 = A.yy * C.yx;    // (bd, bc)
+    return addsub(t1, t2);        // (ac - bd, ad + bc)
+}
+// A * conj(C) as the reference rounds it: (a*c - b*(-d), a*(-d) + b*c).  Since
+// b*(-d) == -(b*d) and a*(-d) == -(a*d) exactly, that is (ac + bd, -(ad) + bc):
+// the same two packed products and ONE packed add with the high half of t1 negated.
+__device__ __forceinline__ f2 cmulc(f2 A, f2 C) {
+    const f2 t1 = A.xx * C;       // (ac, ad)
+    const f2 t2 = A.yy * C.yx;    // (bd, bc)
+    f2 r;
+    asm("v_pk_add_f32 %0, %1, %2 neg_hi:[1,0]" : "=v"(r) : "v"(t1), "v"(t2));
+    return r;
+}
+// a + conj(b) = (a.x + b.x, a.y + (-b.y)), one packed add
+__device__ __forceinline__ f2 addc(f2 a, f2 b) {
+    f2 r;
+    asm("v_pk_add_f32 %0, %1, %2 neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ f2 conj2(f2 A) { return f2{A.x, -A.y}; }
+
 struct Kal {
-    float eqr[5], eqi[5];    // eq_coeff     src/kalman.c:19
-    float gr[5], gi[5];      // kalman_gain  src/kalman.c:20
-    float ur[5][5], ui[5][5];// u (upper triangle used)  src/kalman.c:25
-    float d[5];              // src/kalman.c:29
+    f2 eq[5];                // eq_coeff     src/kalman.c:19
+    f2 g[5];                 // kalman_gain  src/kalman.c:20
+    f2 u[10];                // u[i][j], i < j (src/kalman.c:25), index uix(i, j)
+    f2 d[5];                 // src/kalman.c:29, kept as (d, d) for packed g = f*d
 };
 
+__host__ __device__ constexpr int uix(int i, int j) { return j * (j - 1) / 2 + i; }
+
 // kalman_calculate (src/kalman.c:85-141) then update_eq (src/equalizer.c:25-40)
-__device__ __forceinline__ void update_eq(Kal& k, const float (&xr)[5], const float (&xi)[5],
-                                          float er, float ei) {
+__device__ __forceinline__ void update_eq(Kal& k, const f2 (&x)[5], f2 e) {
     const float E = QK_KAL_E, q = QK_KAL_Q;
-    float fr[5], fi[5], a[5];
-    fr[0] = xr[0];                              // 6.2  f0 = conj(x0)
-    fi[0] = -xi[0];
+    f2 f[5];
+    float a[5];
+    f[0] = conj2(x[0]);                                   // 6.2  f0 = conj(x0)
 #pragma unroll
     for (int j = 1; j < 5; j++) {
         // u0j*conj(x0) + conj(xj) (the double conj() sum rounds to the fp32 sum)
-        float pr = k.ur[0][j] * xr[0] - k.ui[0][j] * (-xi[0]);
-        float pi = k.ur[0][j] * (-xi[0]) + k.ui[0][j] * xr[0];
-        fr[j] = pr + xr[j];
-        fi[j] = pi + (-xi[j]);
+        f[j] = addc(cmulc(k.u[uix(0, j)], x[0]), x[j]);
 #pragma unroll
-        for (int i = 1; i < j; i++) {
-            pr = k.ur[i][j] * xr[i] - k.ui[i][j] * (-xi[i]);
-            pi = k.ur[i][j] * (-xi[i]) + k.ui[i][j] * xr[i];
-            fr[j] = fr[j] + pr;
-            fi[j] = fi[j] + pi;
-        }
+        for (int i = 1; i < j; i++) f[j] = f[j] + cmulc(k.u[uix(i, j)], x[i]);
     }
 #pragma unroll
-    for (int j = 0; j < 5; j++) {               // 6.4  g = f*d
-        k.gr[j] = fr[j] * k.d[j];
-        k.gi[j] = fi[j] * k.d[j];
-    }
-    a[0] = E + (k.gr[0] * fr[0] - k.gi[0] * (-fi[0]));   // 6.5
+    for (int j = 0; j < 5; j++) k.g[j] = f[j] * k.d[j];   // 6.4  g = f*d (both halves d)
 #pragma unroll
-    for (int j = 1; j < 5; j++) a[j] = a[j - 1] + (k.gr[j] * fr[j] - k.gi[j] * (-fi[j]));
-    const float hq = 1.0f + q;                  // 6.7
+    for (int j = 0; j < 5; j++) {                         // 6.5/6.6 Re(g * conj(f))
+        // gr*fr - gi*(-fi) == gr*fr + gi*fi (gi*(-fi) == -(gi*fi) exactly)
+        const f2 t = k.g[j] * f[j];
+        a[j] = (j == 0 ? E : a[j - 1]) + (t.x + t.y);
+    }
+    const float hq = 1.0f + q;                            // 6.7
     const float ht = a[4] * q;
-    float y = 1.0f / (a[0] + ht);               // 6.19 (correctly rounded)
-    k.d[0] = k.d[0] * ((hq * (E + ht)) * y);    // 6.20
+    float y = 1.0f / (a[0] + ht);                         // 6.19 (correctly rounded)
+    k.d[0] = k.d[0] * ((hq * (E + ht)) * y);              // 6.20 (both halves)
 #pragma unroll
     for (int j = 1; j < 5; j++) {
-        const float B = a[j - 1] + ht;          // 6.21
-        const float hr = (-fr[j]) * y;          // 6.11
-        const float hi = (-fi[j]) * y;
-        y = 1.0f / (a[j] + ht);                 // 6.22
-        k.d[j] = k.d[j] * ((hq * B) * y);       // 6.13
+        const float B = a[j - 1] + ht;                    // 6.21
+        const f2 h = (-f[j]) * y;                         // 6.11
+        y = 1.0f / (a[j] + ht);                           // 6.22
+        k.d[j] = k.d[j] * ((hq * B) * y);                 // 6.13
 #pragma unroll
         for (int i = 0; i < j; i++) {
-            const float b1r = k.ur[i][j], b1i = k.ui[i][j];
-            const float cgr = k.gr[i], cgi = -k.gi[i];
-            k.ur[i][j] = b1r + (hr * cgr - hi * cgi);           // 6.15
-            k.ui[i][j] = b1i + (hr * cgi + hi * cgr);
-            k.gr[i] = k.gr[i] + (k.gr[j] * b1r - k.gi[j] * (-b1i));  // 6.16
-            k.gi[i] = k.gi[i] + (k.gr[j] * (-b1i) + k.gi[j] * b1r);
+            const f2 B1 = k.u[uix(i, j)];
+            k.u[uix(i, j)] = B1 + cmulc(h, k.g[i]);          // 6.15
+            k.g[i] = k.g[i] + cmulc(k.g[j], B1);             // 6.16
         }
     }
-    // update_eq: error *= kalman_y; eq += error * conj(g)
-    er = er * y;
-    ei = ei * y;
+    e = e * y;                                            // error *= kalman_y
 #pragma unroll
-    for (int i = 0; i < 5; i++) {
-        const float cgr = k.gr[i], cgi = -k.gi[i];
-        k.eqr[i] = k.eqr[i] + (er * cgr - ei * cgi);
-        k.eqi[i] = k.eqi[i] + (er * cgi + ei * cgr);
-    }
+    for (int i = 0; i < 5; i++) k.eq[i] = k.eq[i] + cmulc(e, k.g[i]);
 }
 
-__device__ void back_group(const StepArgs& a, int grp) {
-    const int lane = threadIdx.x & 63;
-    const int ch = grp * QK_GROUP + lane;
-    const bool live = ch < a.nch;
-    const int chs = live ? ch : 0;
-    const int mi = a.mi_rd[chs];
-    const int rt = a.rt_rd[chs];
-    const float2* wp = a.win_rd + (size_t)grp * QK_NWIN * QK_GROUP + lane;
+// Window reads: non-temporal (L1-bypassing) loads, so a line this CU cached two
+// frames ago is never reused after the front wave rewrote it through L2.
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 ldw(const float4* p) {
+    const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+    return make_float4(v.x, v.y, v.z, v.w);
+}
 
+// One frame of the back wave: lane = channel.  Window slots 1..163 hold
+// dec[mi .. mi+162]; read two slots (16 B) every two steps.
+__device__ __forceinline__ void back_frame(const RxArgs& a, int ch, bool live, int n, int mi,
+                                           int rt, const float2* win, int* rt_next) {
+    const float4* wp = reinterpret_cast<const float4*>(win);
     Kal k;                                         // kalman_reset, src/kalman.c:42-55
 #pragma unroll
     for (int i = 0; i < 5; i++) {
-        k.eqr[i] = k.eqi[i] = k.gr[i] = k.gi[i] = 0.0f;
-        k.d[i] = 1.0f;
-#pragma unroll
-        for (int j = 0; j < 5; j++) k.ur[i][j] = k.ui[i][j] = 0.0f;
+        k.eq[i] = k.g[i] = f2{0.0f, 0.0f};
+        k.d[i] = f2{1.0f, 1.0f};
     }
-    float xr[5], xi[5];
 #pragma unroll
-    for (int i = 0; i < 5; i++) {
-        const float2 v = wp[(size_t)i * QK_GROUP];
-        xr[i] = v.x;
-        xi[i] = v.y;
+    for (int i = 0; i < 10; i++) k.u[i] = f2{0.0f, 0.0f};
+    f2 x[5];
+    {
+        const float4 w0 = ldw(wp + 0), w1 = ldw(wp + 1), w2 = ldw(wp + 2);
+        x[0] = f2{w0.z, w0.w};
+        x[1] = f2{w1.x, w1.y};
+        x[2] = f2{w1.z, w1.w};
+        x[3] = f2{w2.x, w2.y};
+        x[4] = f2{w2.z, w2.w};
     }
     // equalize(): 128 x train_eq (src/qpsk.c:111-123, src/equalizer.c:45-58)
+    const f2* wp2 = reinterpret_cast<const f2*>(win);
     int matches = 0;
     for (int i = 0; i < QK_NPRE; i++) {
-        const float2 nx = wp[(size_t)(i + 5) * QK_GROUP];  // next window sample
+        const f2 nx = __builtin_nontemporal_load(wp2 + i + 6);   // slot i+6 (next step)
         const unsigned long long m = i < 64 ? kPreLo : kPreHi;
         const float ref = ((m >> (i & 63)) & 1ull) ? 1.0f : -1.0f;
-        float vr = 0.0f, vi = 0.0f;
+        f2 v = {0.0f, 0.0f};
 #pragma unroll
-        for (int t = 0; t < 5; t++) {
-            vr = vr + (xr[t] * k.eqr[t] - xi[t] * k.eqi[t]);
-            vi = vi + (xr[t] * k.eqi[t] + xi[t] * k.eqr[t]);
-        }
-        const float er = ref - vr;                 // conjf(ref - val) = (ref-vr, vi)
-        update_eq(k, xr, xi, er, vi);
+        for (int t = 0; t < 5; t++) v = v + cmul(x[t], k.eq[t]);
+        const float er = ref - v.x;                // conjf(ref - val) = (ref - vr, vi)
+        update_eq(k, x, f2{er, v.y});
         if (er * ref > 0.0f) matches++;
 #pragma unroll
-        for (int t = 0; t < 4; t++) { xr[t] = xr[t + 1]; xi[t] = xi[t + 1]; }
-        xr[4] = nx.x;
-        xi[4] = nx.y;
+        for (int t = 0; t < 4; t++) x[t] = x[t + 1];
+        x[4] = nx;
     }
     const bool valid = live && matches > QK_MATCH_MIN;   // src/qpsk.c:196
-    const size_t cf = (size_t)chs * a.F + a.n;
+    const size_t cf = (size_t)ch * a.F + n;
     uint16_t* bo = reinterpret_cast<uint16_t*>(a.bits + cf * QK_NBITS);
     float2* so = a.soft ? a.soft + cf * QK_NDSYM : nullptr;
+    const unsigned long long ks = a.ks[(a.g0 + (unsigned)n) % QK_KS_FRAMES];
     // data symbols (src/qpsk.c:204-215): data_eq + qpsk_demod + scramble
-    for (int s = 0; s < QK_NDSYM; s++) {
-        uint16_t out = 0;
-        float sr = 0.0f, si = 0.0f;
-        if (valid) {
-            const float2 nx = wp[(size_t)(QK_NPRE + s + 5 < QK_NWIN ? QK_NPRE + s + 5 : QK_NWIN - 1) * QK_GROUP];
+    for (int s = 0; s < QK_NDSYM; s += 2) {
+        float4 nx = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (valid) nx = ldw(wp + ((134 + s) >> 1));   // slots 134+s, 135+s
 #pragma unroll
-            for (int t = 0; t < 5; t++) {          // symbol = sum x * conj(eq)
-                sr = sr + (xr[t] * k.eqr[t] - xi[t] * (-k.eqi[t]));
-                si = si + (xr[t] * (-k.eqi[t]) + xi[t] * k.eqr[t]);
+        for (int h = 0; h < 2; h++) {
+            const int ss = s + h;
+            if (ss < QK_NDSYM) {
+                uint16_t out = 0;
+                f2 sy = {0.0f, 0.0f};
+                if (valid) {
+#pragma unroll
+                    for (int t = 0; t < 5; t++) sy = sy + cmulc(x[t], k.eq[t]);
+                    const int dI = sy.x < 0.0f, dQ = sy.y < 0.0f;
+                    const f2 cst = {dI ? -1.0f : 1.0f, dQ ? -1.0f : 1.0f};
+                    update_eq(k, x, (cst - sy) * 0.1f);
+                    const int q = dQ ^ (int)((ks >> (2 * ss)) & 1ull);
+                    const int ib = dI ^ (int)((ks >> (2 * ss + 1)) & 1ull);
+                    out = (uint16_t)(q | (ib << 8));   // bits[2s] = Q, bits[2s+1] = I
+#pragma unroll
+                    for (int t = 0; t < 4; t++) x[t] = x[t + 1];
+                    x[4] = h ? f2{nx.z, nx.w} : f2{nx.x, nx.y};
+                }
+                if (live) {
+                    bo[ss] = out;
+                    if (so) so[ss] = make_float2(sy.x, sy.y);
+                }
             }
-            const int dI = sr < 0.0f, dQ = si < 0.0f;
-            const float cr = dI ? -1.0f : 1.0f, cq = dQ ? -1.0f : 1.0f;
-            update_eq(k, xr, xi, (cr - sr) * 0.1f, (cq - si) * 0.1f);
-            const int q = dQ ^ (int)((a.ks >> (2 * s)) & 1ull);
-            const int ib = dI ^ (int)((a.ks >> (2 * s + 1)) & 1ull);
-            out = (uint16_t)(q | (ib << 8));       // bits[2s] = Q, bits[2s+1] = I
-#pragma unroll
-            for (int t = 0; t < 4; t++) { xr[t] = xr[t + 1]; xi[t] = xi[t + 1]; }
-            xr[4] = nx.x;
-            xi[4] = nx.y;
-        }
-        if (live) {
-            bo[s] = out;
-            if (so) so[s] = make_float2(sr, si);
         }
     }
+    const int rtn = valid ? mi + QK_NPRE : rt;    // src/qpsk.c:219
+    *rt_next = rtn;
     if (live) {
-        const int rt_next = valid ? mi + QK_NPRE : rt;  // src/qpsk.c:219
-        a.rt_wr[ch] = rt_next;
         a.valid[cf] = valid ? 1 : 0;
-        if (a.trace) {
-            int4* tp = reinterpret_cast<int4*>(a.trace + cf * 4);
-            *tp = make_int4(mi, matches, valid ? 1 : 0, rt_next);
+        if (a.trace)
+            *reinterpret_cast<int4*>(a.trace + cf * 4) = make_int4(mi, matches, valid ? 1 : 0, rtn);
+    }
+}
+
+// Plain pointer parameters (not a by-value struct): the compiler then knows every
+// pointer is a global-memory pointer (global_load/store, no flat) and nothing of
+// the argument block is indexed dynamically (no scratch copy).
+// 12 waves per workgroup, 3 per SIMD (<= 168 VGPRs), one workgroup per CU (LDS).
+__global__ void __launch_bounds__(kBlock, 3) rx_kernel(
+    const int16_t* in, int16_t* hist, const float2* ptab, const unsigned long long* ks,
+    float2* win0, float2* win1, int* mi0, int* mi1, int* rt0, int* rt1, uint8_t* bits,
+    uint8_t* valid, int32_t* trace, float2* soft, int nch, int F, unsigned g0, int roles) {
+    const RxArgs a{in, hist, ptab, ks, win0, win1, mi0, mi1, rt0, rt1, bits, valid, trace, soft,
+                   nch, F, g0, roles};
+    __shared__ __attribute__((aligned(16))) float2 P[QK_FRAME];
+    __shared__ __attribute__((aligned(16))) float2 Ms[kFrontWaves][kM];
+    __shared__ __attribute__((aligned(16))) float2 decs[kFrontWaves][2][kDec];
+    __shared__ int mi_s[kGroups][2][QK_GROUP], rt_s[kGroups][2][QK_GROUP];
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int grp0 = blockIdx.x * kGroups;
+    for (int i = threadIdx.x; i < QK_FRAME / 2; i += kBlock)
+        reinterpret_cast<float4*>(P)[i] = reinterpret_cast<const float4*>(a.ptab)[i];
+    if (wave < kGroups) {   // per-channel state of the groups at the call's first frame
+        const int ch = (grp0 + wave) * QK_GROUP + lane;
+        if (ch < a.nch) {
+            mi_s[wave][0][lane] = mi_of(a, a.g0)[ch];
+            rt_s[wave][0][lane] = rt_of(a, a.g0)[ch];
         }
     }
-}
-
-__global__ void __launch_bounds__(kBlock) rx_step_kernel(StepArgs a) {
-    __shared__ float2 lds[kWaves * kLdsWave];
-    const int b = blockIdx.x;
-    if (b < a.nb_back) {
-        const int grp = b * kWaves + (threadIdx.x >> 6);
-        if (grp * QK_GROUP < a.nch) back_group(a, grp);
+    __syncthreads();
+    if (wave < kGroups) {
+        // ------------------------------------------------------------ back
+        const int gi = wave;
+        const int ch = (grp0 + gi) * QK_GROUP + lane;
+        const bool live = ch < a.nch;
+        const bool any = (grp0 + gi) * QK_GROUP < a.nch;
+        if (((a.roles >> 4) & 3) == 2) __builtin_amdgcn_s_setprio(2);
+        for (int n = 0; n < a.F; n++) {
+            const int p = n & 1;
+            if (any && (a.roles & 1))
+                back_frame(a, live ? ch : 0, live, n, mi_s[gi][p][lane], rt_s[gi][p][lane],
+                           win_of(a, a.g0 + (unsigned)n) + (size_t)(live ? ch : 0) * kWinStride,
+                           &rt_s[gi][p ^ 1][lane]);
+            else
+                rt_s[gi][p ^ 1][lane] = rt_s[gi][p][lane];
+            __syncthreads();
+        }
+        if (live) {   // per-channel state after the call's last frame
+            const unsigned ge = a.g0 + (unsigned)a.F;
+            mi_of(a, ge)[ch] = mi_s[gi][a.F & 1][lane];
+            rt_of(a, ge)[ch] = rt_s[gi][a.F & 1][lane];
+        }
     } else {
-        front_group(a, b - a.nb_back, lds);
-    }
-}
-
-// carry the samples the next call needs: x_{N-1}[0..1191], x_{N-1}[1832..1879],
-// x_{N-2}[1832..1879] (eight-sample units)
-__global__ void hist_kernel(const int16_t* in, int16_t* hist, int nch, int F) {
-    const int ch = blockIdx.x;
-    if (ch >= nch) return;
-    int16_t* h0 = hist + (size_t)ch * 2 * QK_FRAME;
-    int16_t* h1 = h0 + QK_FRAME;
-    const int16_t* last = in + ((size_t)ch * F + (F - 1)) * QK_FRAME;
-    const int16_t* prev = F >= 2 ? in + ((size_t)ch * F + (F - 2)) * QK_FRAME : h1;
-    for (int u = threadIdx.x; u < 6; u += blockDim.x) {
-        const int t = 1832 + 8 * u;
-        *reinterpret_cast<int4*>(h0 + t) = *reinterpret_cast<const int4*>(prev + t);
-    }
-    __syncthreads();  // F == 1 reads h1 before it is overwritten
-    for (int u = threadIdx.x; u < 155; u += blockDim.x) {
-        const int t = u < 149 ? 8 * u : 1832 + 8 * (u - 149);
-        *reinterpret_cast<int4*>(h1 + t) = *reinterpret_cast<const int4*>(last + t);
+        // ------------------------------------------------------------ front
+        // channel by channel: mix (prefetched samples) -> store the previous
+        // channel's window -> prefetch the next channel -> FIR/correlate/argmax
+        const int f = wave - kGroups;
+        const int gi = f / kFrontPer;
+        const int cbeg = (f % kFrontPer) * kFrontCh;
+        const int ch0 = (grp0 + gi) * QK_GROUP + cbeg;
+        const int nlive = max(0, min(kFrontCh, a.nch - ch0));
+        float2* M = Ms[f];
+        int pf[kPf];
+        const bool on = (a.roles & 2) != 0 && nlive > 0;
+        if (((a.roles >> 4) & 3) == 1) __builtin_amdgcn_s_setprio(2);
+        if (on) prefetch(srcs(a, ch0, 0), lane, pf);
+        for (int n = 0; n < a.F; n++) {
+            const int p = n & 1;
+            const unsigned g = a.g0 + (unsigned)n;
+            float2* wout = win_of(a, g + 1u);
+            int pmi = 0;
+            for (int c = 0; on && c < nlive; c++) {
+                const int ch = ch0 + c;
+                float2* dcur = decs[f][c & 1];
+                mix(lane, pf, g, P, M);
+                if (c > 0) store_window(lane, pmi, decs[f][(c - 1) & 1], wout + (size_t)(ch - 1) * kWinStride);
+                if (c + 1 < nlive) prefetch(srcs(a, ch + 1, n), lane, pf);
+                else if (n + 1 < a.F) prefetch(srcs(a, ch0, n + 1), lane, pf);
+                wave_lds_sync();
+                pmi = front_channel(lane, rt_s[gi][p][cbeg + c], M, dcur);
+                if (lane == 0) mi_s[gi][p ^ 1][cbeg + c] = pmi;
+                if (c + 1 == nlive) store_window(lane, pmi, dcur, wout + (size_t)ch * kWinStride);
+                wave_lds_sync();
+            }
+            __syncthreads();
+        }
+        // carry the samples the next call needs: x_{F-1}[0..1191], x_{F-1}[1832..1879],
+        // x_{F-2}[1832..1879]
+        for (int c = 0; c < nlive; c++) {
+            const int ch = ch0 + c;
+            int16_t* h0 = a.hist + (size_t)ch * 2 * QK_FRAME;
+            int16_t* h1 = h0 + QK_FRAME;
+            const int16_t* last = frame_ptr(a, ch, a.F - 1);
+            const int16_t* prev = frame_ptr(a, ch, a.F - 2);
+            if (lane < 6) {   // F == 1: prev is h1; its load completes before the h1 stores
+                const int t = 1832 + 8 * lane;
+                *reinterpret_cast<int4*>(h0 + t) = *reinterpret_cast<const int4*>(prev + t);
+            }
+            for (int u = lane; u < 155; u += 64) {
+                const int t = u < 149 ? 8 * u : 1832 + 8 * (u - 149);
+                *reinterpret_cast<int4*>(h1 + t) = *reinterpret_cast<const int4*>(last + t);
+            }
+        }
     }
 }
 
@@ -385,11 +599,11 @@ struct qpsk_ctx {
     uint64_t frames = 0;
     hipStream_t stream = nullptr;
     float2* d_ptab = nullptr;
+    unsigned long long* d_ks = nullptr;
     int16_t* d_hist = nullptr;
     float2* d_win[2] = {nullptr, nullptr};
     int* d_mi[2] = {nullptr, nullptr};
     int* d_rt[2] = {nullptr, nullptr};
-    unsigned long long ks[QK_KS_FRAMES];
     // staging for the host-memory entry point
     int16_t* s_in = nullptr;
     uint8_t* s_bits = nullptr;
@@ -397,14 +611,15 @@ struct qpsk_ctx {
     int32_t* s_trace = nullptr;
     float* s_soft = nullptr;
     size_t s_frames = 0;
-    // kernel-span accounting: events around each call's step-kernel sequence
+    // kernel-span accounting: events around each call's kernel
     static constexpr int kEv = 64;
     hipEvent_t ev[kEv][2] = {};
-    int ev_launches[kEv] = {};
+    int ev_frames[kEv] = {};
     int ev_n = 0;
     bool timing = false;
+    int roles = 3 | (1 << 4);   // roles + priority; QPSK_ABLATE / QPSK_PRIO (profiling)
     float pend_ms = 0.0f;
-    int pend_launches = 0;
+    int pend_frames = 0;
 };
 
 extern "C" int qpsk_rx_timing_collect(qpsk_ctx* c, float* ms, int* launches);
@@ -412,7 +627,7 @@ extern "C" int qpsk_rx_timing_collect(qpsk_ctx* c, float* ms, int* launches);
 static int herr(hipError_t e) { return e == hipSuccess ? QPSK_OK : QPSK_EHIP - (int)e; }
 #define HCHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) return herr(e_); } while (0)
 
-static void build_tables(qpsk_ctx* c, float2* ptab) {
+static void build_tables(float2* ptab, unsigned long long* ksf) {
     // P[t] = R^(t+1): fbb_rx_phase *= fbb_rx_rect (src/qpsk.c:139), fp32, host
     const float rr = bits2f(QK_RX_RECT_RE_BITS), ri = bits2f(QK_RX_RECT_IM_BITS);
     volatile float pr = 1.0f, pi = 0.0f;  // volatile: keep every op a rounded fp32 op
@@ -435,18 +650,23 @@ static void build_tables(qpsk_ctx* c, float2* ptab) {
         unsigned long long w = 0;
         for (int b = 0; b < QK_NBITS; b++)
             w |= (unsigned long long)ks[(62 * f + b) % QK_KS_PERIOD] << b;
-        c->ks[f] = w;
+        ksf[f] = w;
     }
 }
 
+// state arrays cover whole workgroups (kGroups groups of 64 channels)
+static size_t nslot(const qpsk_ctx* c) {
+    return (size_t)((c->ngroup + kGroups - 1) / kGroups) * kGroups * QK_GROUP;
+}
+
 static int ctx_alloc(qpsk_ctx* c) {
-    const size_t nslot = (size_t)c->ngroup * QK_GROUP;
     HCHECK(hipMalloc(&c->d_ptab, sizeof(float2) * QK_FRAME));
-    HCHECK(hipMalloc(&c->d_hist, sizeof(int16_t) * nslot * 2 * QK_FRAME));
+    HCHECK(hipMalloc(&c->d_ks, sizeof(unsigned long long) * QK_KS_FRAMES));
+    HCHECK(hipMalloc(&c->d_hist, sizeof(int16_t) * nslot(c) * 2 * QK_FRAME));
     for (int p = 0; p < 2; p++) {
-        HCHECK(hipMalloc(&c->d_win[p], sizeof(float2) * (size_t)c->ngroup * QK_NWIN * QK_GROUP));
-        HCHECK(hipMalloc(&c->d_mi[p], sizeof(int) * nslot));
-        HCHECK(hipMalloc(&c->d_rt[p], sizeof(int) * nslot));
+        HCHECK(hipMalloc(&c->d_win[p], sizeof(float2) * nslot(c) * kWinStride));
+        HCHECK(hipMalloc(&c->d_mi[p], sizeof(int) * nslot(c)));
+        HCHECK(hipMalloc(&c->d_rt[p], sizeof(int) * nslot(c)));
     }
     return QPSK_OK;
 }
@@ -454,18 +674,17 @@ static int ctx_alloc(qpsk_ctx* c) {
 extern "C" int qpsk_rx_reset(qpsk_ctx* c) {
     if (!c) return QPSK_EINVAL;
     HCHECK(hipSetDevice(c->device));
-    const size_t nslot = (size_t)c->ngroup * QK_GROUP;
-    HCHECK(hipMemsetAsync(c->d_hist, 0, sizeof(int16_t) * nslot * 2 * QK_FRAME, c->stream));
+    const size_t ns = nslot(c);
+    HCHECK(hipMemsetAsync(c->d_hist, 0, sizeof(int16_t) * ns * 2 * QK_FRAME, c->stream));
     for (int p = 0; p < 2; p++) {
-        HCHECK(hipMemsetAsync(c->d_win[p], 0, sizeof(float2) * (size_t)c->ngroup * QK_NWIN * QK_GROUP,
-                              c->stream));
-        HCHECK(hipMemsetAsync(c->d_mi[p], 0, sizeof(int) * nslot, c->stream));
+        HCHECK(hipMemsetAsync(c->d_win[p], 0, sizeof(float2) * ns * kWinStride, c->stream));
+        HCHECK(hipMemsetAsync(c->d_mi[p], 0, sizeof(int) * ns, c->stream));
     }
-    int* rt0 = (int*)malloc(sizeof(int) * nslot);
+    int* rt0 = (int*)malloc(sizeof(int) * ns);
     if (!rt0) return QPSK_ENOMEM;
-    for (size_t i = 0; i < nslot; i++) rt0[i] = QK_RT0;
-    hipError_t e = hipMemcpy(c->d_rt[0], rt0, sizeof(int) * nslot, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(c->d_rt[1], rt0, sizeof(int) * nslot, hipMemcpyHostToDevice);
+    for (size_t i = 0; i < ns; i++) rt0[i] = QK_RT0;
+    hipError_t e = hipMemcpy(c->d_rt[0], rt0, sizeof(int) * ns, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(c->d_rt[1], rt0, sizeof(int) * ns, hipMemcpyHostToDevice);
     free(rt0);
     HCHECK(e);
     HCHECK(hipStreamSynchronize(c->stream));
@@ -478,6 +697,7 @@ static void ctx_free(qpsk_ctx* c) {
         for (int j = 0; j < 2; j++)
             if (c->ev[i][j]) (void)hipEventDestroy(c->ev[i][j]);
     (void)hipFree(c->d_ptab);
+    (void)hipFree(c->d_ks);
     (void)hipFree(c->d_hist);
     for (int p = 0; p < 2; p++) {
         (void)hipFree(c->d_win[p]);
@@ -506,13 +726,23 @@ extern "C" qpsk_ctx* qpsk_rx_create(int device, int nch, int* err) {
     c->device = device;
     c->nch = nch;
     c->ngroup = (nch + QK_GROUP - 1) / QK_GROUP;
+    if (const char* ab = getenv("QPSK_ABLATE")) {   // timing experiments; output invalid
+        if (!strcmp(ab, "front")) c->roles = (c->roles & ~3) | 2;
+        else if (!strcmp(ab, "back")) c->roles = (c->roles & ~3) | 1;
+    }
+    if (const char* pr = getenv("QPSK_PRIO")) {     // issue-priority experiments
+        const int v = !strcmp(pr, "front") ? 1 : !strcmp(pr, "back") ? 2 : 0;
+        c->roles = (c->roles & 3) | (v << 4);
+    }
     int r = herr(hipSetDevice(device));
     if (r == QPSK_OK) r = herr(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     if (r == QPSK_OK) r = ctx_alloc(c);
     if (r == QPSK_OK) {
-        float2 ptab[QK_FRAME];
-        build_tables(c, ptab);
+        static float2 ptab[QK_FRAME];
+        static unsigned long long ksf[QK_KS_FRAMES];
+        build_tables(ptab, ksf);
         r = herr(hipMemcpy(c->d_ptab, ptab, sizeof ptab, hipMemcpyHostToDevice));
+        if (r == QPSK_OK) r = herr(hipMemcpy(c->d_ks, ksf, sizeof ksf, hipMemcpyHostToDevice));
     }
     if (r == QPSK_OK) r = qpsk_rx_reset(c);
     if (r != QPSK_OK) {
@@ -541,20 +771,9 @@ extern "C" int qpsk_rx_batch_device(qpsk_ctx* c, const int16_t* d_in, int F, uin
                                     void* stream) {
     if (!c || F < 0 || (F > 0 && (!d_in || !d_bits || !d_valid))) return QPSK_EINVAL;
     if (F == 0) return QPSK_OK;
+    if ((reinterpret_cast<uintptr_t>(d_in) & 15u) != 0) return QPSK_EINVAL;  // int4 loads
     HCHECK(hipSetDevice(c->device));
     hipStream_t s = (hipStream_t)stream;
-    const int nb_back = (c->ngroup + kWaves - 1) / kWaves;
-    StepArgs a{};
-    a.in = d_in;
-    a.hist = c->d_hist;
-    a.ptab = c->d_ptab;
-    a.bits = d_bits;
-    a.valid = d_valid;
-    a.trace = d_trace;
-    a.soft = reinterpret_cast<float2*>(d_soft);
-    a.nch = c->nch;
-    a.F = F;
-    a.nb_back = nb_back;
     int slot = -1;
     if (c->timing) {
         if (c->ev_n == qpsk_ctx::kEv) {   // pool full: fold pending spans into the totals
@@ -563,32 +782,22 @@ extern "C" int qpsk_rx_batch_device(qpsk_ctx* c, const int16_t* d_in, int F, uin
             int r = qpsk_rx_timing_collect(c, &ms, &l);
             if (r != QPSK_OK) return r;
             c->pend_ms += ms;
-            c->pend_launches += l;
+            c->pend_frames += l;
         }
         slot = c->ev_n++;
         for (int j = 0; j < 2; j++)
             if (!c->ev[slot][j]) HCHECK(hipEventCreate(&c->ev[slot][j]));
         HCHECK(hipEventRecord(c->ev[slot][0], s));
-        c->ev_launches[slot] = F;
+        c->ev_frames[slot] = F;
     }
-    for (int n = 0; n < F; n++) {
-        const uint64_t g = c->frames + (uint64_t)n;
-        const int p = (int)(g & 1u);
-        a.n = n;
-        a.g = (unsigned)(g & 0xffffffffu);
-        a.ks = c->ks[g % QK_KS_FRAMES];
-        a.win_rd = c->d_win[p];
-        a.win_wr = c->d_win[p ^ 1];
-        a.mi_rd = c->d_mi[p];
-        a.mi_wr = c->d_mi[p ^ 1];
-        a.rt_rd = c->d_rt[p];
-        a.rt_wr = c->d_rt[p ^ 1];
-        hipLaunchKernelGGL(rx_step_kernel, dim3(nb_back + c->ngroup), dim3(kBlock), 0, s, a);
-        HCHECK(hipGetLastError());
-    }
-    if (slot >= 0) HCHECK(hipEventRecord(c->ev[slot][1], s));
-    hipLaunchKernelGGL(hist_kernel, dim3(c->nch), dim3(64), 0, s, d_in, c->d_hist, c->nch, F);
+    hipLaunchKernelGGL(rx_kernel, dim3((c->ngroup + kGroups - 1) / kGroups), dim3(kBlock), 0, s,
+                       d_in, c->d_hist,
+                       c->d_ptab, c->d_ks, c->d_win[0], c->d_win[1], c->d_mi[0], c->d_mi[1],
+                       c->d_rt[0], c->d_rt[1], d_bits, d_valid, d_trace,
+                       reinterpret_cast<float2*>(d_soft), c->nch, F,
+                       (unsigned)(c->frames & 0xffffffffu), c->roles);
     HCHECK(hipGetLastError());
+    if (slot >= 0) HCHECK(hipEventRecord(c->ev[slot][1], s));
     c->frames += (uint64_t)F;
     return QPSK_OK;
 }
@@ -599,23 +808,23 @@ extern "C" int qpsk_rx_timing_enable(qpsk_ctx* c, int on) {
     return QPSK_OK;
 }
 
-extern "C" int qpsk_rx_timing_collect(qpsk_ctx* c, float* ms, int* launches) {
-    if (!c || !ms || !launches) return QPSK_EINVAL;
+extern "C" int qpsk_rx_timing_collect(qpsk_ctx* c, float* ms, int* frames) {
+    if (!c || !ms || !frames) return QPSK_EINVAL;
     HCHECK(hipSetDevice(c->device));
     float tot = c->pend_ms;
-    int nl = c->pend_launches;
+    int nf = c->pend_frames;
     for (int i = 0; i < c->ev_n; i++) {
         HCHECK(hipEventSynchronize(c->ev[i][1]));
         float t = 0.0f;
         HCHECK(hipEventElapsedTime(&t, c->ev[i][0], c->ev[i][1]));
         tot += t;
-        nl += c->ev_launches[i];
+        nf += c->ev_frames[i];
     }
     c->ev_n = 0;
     c->pend_ms = 0.0f;
-    c->pend_launches = 0;
+    c->pend_frames = 0;
     *ms = tot;
-    *launches = nl;
+    *frames = nf;
     return QPSK_OK;
 }
 
