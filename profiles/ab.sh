@@ -1,0 +1,11 @@
+#!/bin/bash
+# A/B in ONE process-free sequence on one device: bench each library variant,
+# interleaved, R rounds.  usage: bash profiles/ab.sh R lib1 lib2 ...
+R=$1; shift
+for r in $(seq 1 $R); do
+  for lib in "$@"; do
+    QPSK_LIB=$lib timeout -k 10 300 python bench.py --cpu-channels 0 --verify 0 --steps 3 --warmup 1 \
+      | python -c "import sys,json; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); print('$lib', d['ms_per_step'])" \
+      || exit 1
+  done
+done

@@ -17,7 +17,8 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libqpsk_hip.so")
+# QPSK_LIB overrides the library path (A/B experiments with variant builds only)
+LIB_PATH = os.environ.get("QPSK_LIB") or os.path.join(HERE, "libqpsk_hip.so")
 
 FRAME_SIZE = 1880        # headers/qpsk_internal.h:45
 DATA_SYMBOLS = 31        # headers/qpsk_internal.h:37

@@ -28,6 +28,7 @@
 
 #include "qpsk_batch.h"
 #include "qpsk_consts.h"
+#include "qpsk_rcp.h"
 
 #pragma clang fp contract(off)
 
@@ -80,6 +81,27 @@ struct RxArgs {
     int roles;               // bit 0: back, bit 1: front (3 in production); bits 4-5:
                              // issue priority boost (0 none, 1 front, 2 back)
 };
+
+// Diagnostic build only (-DQPSK_STAMPS): per-phase cycle sums of the front
+// wave, read back with qpsk_debug_stamps().  In the product build every stamp
+// is compiled out.
+#ifdef QPSK_STAMPS
+__device__ unsigned long long g_stamps[16];
+#define STAMP_DECL unsigned long long st_acc[16] = {}; unsigned long long st_t0 = stamp_now();
+#define STAMP(i) do { const unsigned long long t_ = stamp_now(); st_acc[i] += t_ - st_t0; st_t0 = t_; } while (0)
+#define STAMP_FLUSH() do { if (lane == 0) for (int i_ = 0; i_ < 16; i_++) atomicAdd(&g_stamps[i_], st_acc[i_]); } while (0)
+__device__ __forceinline__ unsigned long long stamp_now() {
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#else
+#define STAMP_DECL
+#define STAMP(i) do { } while (0)
+#define STAMP_FLUSH() do { } while (0)
+#endif
 
 __device__ __forceinline__ float2* win_of(const RxArgs& a, unsigned g) { return (g & 1u) ? a.win1 : a.win0; }
 __device__ __forceinline__ int* mi_of(const RxArgs& a, unsigned g) { return (g & 1u) ? a.mi1 : a.mi0; }
@@ -182,10 +204,28 @@ __device__ __forceinline__ unsigned wave_max_u32(unsigned v) {
 }
 
 __device__ __forceinline__ f2 ld2(const float2* p) { return *reinterpret_cast<const f2*>(p); }
+// same, but volatile so the load/store optimizer does not pair it into a
+// ds_read2_b64 (8 LDS cycles per pair vs 2 per ds_read_b64: MI355X_MICROARCH.md)
+typedef __attribute__((address_space(3))) const volatile f2 lds_vf2;
+__device__ __forceinline__ f2 ld2nt(const float2* p) {
+    return *(lds_vf2*)p;   // p points into LDS
+}
 
 // One channel of frame n's front: D_n (decimated with rx_timing rt), F_{n+1},
 // correlation of dec_{n+1} = [D_n, F_{n+1}] and its argmax mi.
-__device__ __forceinline__ int front_channel(int lane, int rt, float2* M, float2* dec) {
+#ifdef QPSK_STAMPS
+#define FSTAMP(i) do { const unsigned long long t_ = stamp_now(); facc[8 + (i)] += t_ - ft0; ft0 = t_; } while (0)
+#define FACC_PARAM , unsigned long long (&facc)[16]
+#define FACC_ARG , st_acc
+#else
+#define FSTAMP(i) do { } while (0)
+#define FACC_PARAM
+#define FACC_ARG
+#endif
+__device__ __forceinline__ int front_channel(int lane, int rt, float2* M, float2* dec FACC_PARAM) {
+#ifdef QPSK_STAMPS
+    unsigned long long ft0 = stamp_now();
+#endif
     // RRC (src/fir.c:36-42), outputs accumulated in tap order.  Decimated
     // outputs D[o] = fir_out[5o + rt] (model A): lane l makes
     // o = 3l..3l+2 from the 59 samples M[15l + rt + s], read in batches.
@@ -197,7 +237,7 @@ __device__ __forceinline__ int front_channel(int lane, int rt, float2* M, float2
             f2 v[15];
 #pragma unroll
             for (int j = 0; j < 15; j++)
-                if (s0 + j < 59) v[j] = ld2(b + s0 + j);
+                if (s0 + j < 59) v[j] = ld2nt(b + s0 + j);
 #pragma unroll
             for (int j = 0; j < 15; j++) {
                 const int s = s0 + j;
@@ -215,6 +255,7 @@ __device__ __forceinline__ int front_channel(int lane, int rt, float2* M, float2
                 dec[3 * lane + m] = make_float2(o.x, o.y);
             }
     }
+    FSTAMP(0);
     // Undecimated head F_{n+1}[j] = fir_out'[j], j < 102: lane l makes j = 2l, 2l+1
     if (lane < 51) {
         const float2* b = M + kM1 + 2 * lane;
@@ -241,28 +282,35 @@ __device__ __forceinline__ int front_channel(int lane, int rt, float2* M, float2
         }
     }
     wave_lds_sync();
-    // p*(dr-di, di+dr) == preambletable[i]*dec[j] exactly (p = +-1); TU reuses M,
-    // even j first so that lane l's term s is at a lane-contiguous position.
+    FSTAMP(1);
+    // p*(dr-di, di+dr) == preambletable[i]*dec[j] exactly (p = +-1); TU reuses M.
     float2* TU = M;
 #pragma unroll
     for (int r = 0; r < 4; r++) {
         const int j = lane + 64 * r;
         if (j < 255) {
             const float2 d = dec[j];
-            TU[(j & 1) ? 128 + (j >> 1) : (j >> 1)] = make_float2(d.x - d.y, d.y + d.x);
+            TU[j] = make_float2(d.x - d.y, d.y + d.x);
         }
     }
     wave_lds_sync();
     // correlate lags 2*lane and 2*lane+1 (src/qpsk.c:88-96), terms in index
     // order; acc = acc +- (T, U) is one packed add
+    FSTAMP(2);
     f2 acc0 = {0.0f, 0.0f}, acc1 = {0.0f, 0.0f};
+    // lane l needs TU[2l + s], s = 0..128: pairs (s, s+1) with s even start at
+    // an even index, so each pair is one aligned, conflict-free ds_read_b128
+    const float4* tp = reinterpret_cast<const float4*>(TU + 2 * lane);
 #pragma unroll
     for (int s0 = 0; s0 <= QK_NPRE; s0 += 16) {
         f2 v[16];
 #pragma unroll
-        for (int j = 0; j < 16; j++) {
-            const int s = s0 + j;
-            if (s <= QK_NPRE) v[j] = ld2(TU + ((s & 1) ? 128 + lane + (s >> 1) : lane + (s >> 1)));
+        for (int j = 0; j < 16; j += 2) {
+            if (s0 + j <= QK_NPRE) {
+                const float4 q = tp[(s0 + j) >> 1];
+                v[j] = f2{q.x, q.y};
+                v[j + 1] = f2{q.z, q.w};
+            }
         }
 #pragma unroll
         for (int j = 0; j < 16; j++) {
@@ -271,6 +319,7 @@ __device__ __forceinline__ int front_channel(int lane, int rt, float2* M, float2
             if (s >= 1 && s <= QK_NPRE) acc1 = QK_PRE[s - 1] > 0 ? acc1 + v[j] : acc1 - v[j];
         }
     }
+    FSTAMP(3);
     const float r0 = acc0.x, i0 = acc0.y, r1 = acc1.x, i1 = acc1.y;
     const float c0 = r0 * r0 + i0 * i0;    // cnormf, src/qpsk.c:75-80
     const float c1 = r1 * r1 + i1 * i1;
@@ -281,6 +330,7 @@ __device__ __forceinline__ int front_channel(int lane, int rt, float2* M, float2
     const unsigned k0 = c0 > 0.0f ? __float_as_uint(c0) : 0u;
     const unsigned k1 = c1 > 0.0f ? __float_as_uint(c1) : 0u;
     const unsigned km = wave_max_u32(max(k0, k1));
+    FSTAMP(4);
     if (km == 0u) return 0;
     const unsigned long long m0 = __ballot(k0 == km), m1 = __ballot(k1 == km);
     const int i0x = m0 ? 2 * (__ffsll((long long)m0) - 1) : 1 << 20;
@@ -370,13 +420,27 @@ __device__ __forceinline__ void update_eq(Kal& k, const f2 (&x)[5], f2 e) {
     }
     const float hq = 1.0f + q;                            // 6.7
     const float ht = a[4] * q;
-    float y = 1.0f / (a[0] + ht);                         // 6.19 (correctly rounded)
+    // the five divisor operands of 6.19 / 6.22; one range check for all of
+    // them (qk_rcp_fast == 1.0f / x inside it, see qpsk_rcp.h)
+    float xs[5], ys[5];
+#pragma unroll
+    for (int j = 0; j < 5; j++) xs[j] = a[j] + ht;
+    const float lo = fminf(fminf(fminf(xs[0], xs[1]), fminf(xs[2], xs[3])), xs[4]);
+    const float hi = fmaxf(fmaxf(fmaxf(xs[0], xs[1]), fmaxf(xs[2], xs[3])), xs[4]);
+    if (__builtin_expect(qk_rcp_in_range(lo, hi), 1)) {
+#pragma unroll
+        for (int j = 0; j < 5; j++) ys[j] = qk_rcp_fast(xs[j]);
+    } else {
+#pragma unroll
+        for (int j = 0; j < 5; j++) ys[j] = qk_div_ieee(xs[j]);
+    }
+    float y = ys[0];                                      // 6.19
     k.d[0] = k.d[0] * ((hq * (E + ht)) * y);              // 6.20 (both halves)
 #pragma unroll
     for (int j = 1; j < 5; j++) {
         const float B = a[j - 1] + ht;                    // 6.21
         const f2 h = (-f[j]) * y;                         // 6.11
-        y = 1.0f / (a[j] + ht);                           // 6.22
+        y = ys[j];                                        // 6.22
         k.d[j] = k.d[j] * ((hq * B) * y);                 // 6.13
 #pragma unroll
         for (int i = 0; i < j; i++) {
@@ -390,13 +454,11 @@ __device__ __forceinline__ void update_eq(Kal& k, const f2 (&x)[5], f2 e) {
     for (int i = 0; i < 5; i++) k.eq[i] = k.eq[i] + cmulc(e, k.g[i]);
 }
 
-// Window reads: non-temporal (L1-bypassing) loads, so a line this CU cached two
-// frames ago is never reused after the front wave rewrote it through L2.
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ float4 ldw(const float4* p) {
-    const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
-    return make_float4(v.x, v.y, v.z, v.w);
-}
+// Window reads are plain loads: the window was stored by the front wave of this
+// workgroup before the frame's __syncthreads(), which makes it visible to the
+// whole workgroup (same CU).  (Non-temporal loads re-fetch each line from L2/HBM
+// per step: 2x the traffic in profiles/calib.)
+__device__ __forceinline__ float4 ldw(const float4* p) { return *p; }
 
 // One frame of the back wave: lane = channel.  Window slots 1..163 hold
 // dec[mi .. mi+162]; read two slots (16 B) every two steps.
@@ -424,7 +486,7 @@ __device__ __forceinline__ void back_frame(const RxArgs& a, int ch, bool live, i
     const f2* wp2 = reinterpret_cast<const f2*>(win);
     int matches = 0;
     for (int i = 0; i < QK_NPRE; i++) {
-        const f2 nx = __builtin_nontemporal_load(wp2 + i + 6);   // slot i+6 (next step)
+        const f2 nx = wp2[i + 6];                  // slot i+6 (next step)
         const unsigned long long m = i < 64 ? kPreLo : kPreHi;
         const float ref = ((m >> (i & 63)) & 1ull) ? 1.0f : -1.0f;
         f2 v = {0.0f, 0.0f};
@@ -496,7 +558,9 @@ __global__ void __launch_bounds__(kBlock, 3) rx_kernel(
     __shared__ __attribute__((aligned(16))) float2 decs[kFrontWaves][2][kDec];
     __shared__ int mi_s[kGroups][2][QK_GROUP], rt_s[kGroups][2][QK_GROUP];
     const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
+    // wave-uniform by construction; readfirstlane tells the compiler, so every
+    // per-wave index and pointer below lives in SGPRs
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int grp0 = blockIdx.x * kGroups;
     for (int i = threadIdx.x; i < QK_FRAME / 2; i += kBlock)
         reinterpret_cast<float4*>(P)[i] = reinterpret_cast<const float4*>(a.ptab)[i];
@@ -544,6 +608,7 @@ __global__ void __launch_bounds__(kBlock, 3) rx_kernel(
         const bool on = (a.roles & 2) != 0 && nlive > 0;
         if (((a.roles >> 4) & 3) == 1) __builtin_amdgcn_s_setprio(2);
         if (on) prefetch(srcs(a, ch0, 0), lane, pf);
+        STAMP_DECL
         for (int n = 0; n < a.F; n++) {
             const int p = n & 1;
             const unsigned g = a.g0 + (unsigned)n;
@@ -553,17 +618,25 @@ __global__ void __launch_bounds__(kBlock, 3) rx_kernel(
                 const int ch = ch0 + c;
                 float2* dcur = decs[f][c & 1];
                 mix(lane, pf, g, P, M);
+                STAMP(0);
                 if (c > 0) store_window(lane, pmi, decs[f][(c - 1) & 1], wout + (size_t)(ch - 1) * kWinStride);
-                if (c + 1 < nlive) prefetch(srcs(a, ch + 1, n), lane, pf);
-                else if (n + 1 < a.F) prefetch(srcs(a, ch0, n + 1), lane, pf);
+                {   // next channel of this frame, else the first of the next frame
+                    const bool same = c + 1 < nlive;
+                    if (same || n + 1 < a.F)
+                        prefetch(srcs(a, same ? ch + 1 : ch0, same ? n : n + 1), lane, pf);
+                }
                 wave_lds_sync();
-                pmi = front_channel(lane, rt_s[gi][p][cbeg + c], M, dcur);
+                STAMP(1);
+                pmi = front_channel(lane, rt_s[gi][p][cbeg + c], M, dcur FACC_ARG);
                 if (lane == 0) mi_s[gi][p ^ 1][cbeg + c] = pmi;
                 if (c + 1 == nlive) store_window(lane, pmi, dcur, wout + (size_t)ch * kWinStride);
                 wave_lds_sync();
+                STAMP(6);
             }
             __syncthreads();
+            STAMP(7);
         }
+        STAMP_FLUSH();
         // carry the samples the next call needs: x_{F-1}[0..1191], x_{F-1}[1832..1879],
         // x_{F-2}[1832..1879]
         for (int c = 0; c < nlive; c++) {
@@ -871,6 +944,18 @@ extern "C" int qpsk_rx_batch(qpsk_ctx* c, const int16_t* in, int F, uint8_t* bit
     HCHECK(hipStreamSynchronize(c->stream));
     return QPSK_OK;
 }
+
+#ifdef QPSK_STAMPS
+extern "C" int qpsk_debug_stamps(unsigned long long* out16, int reset) {
+    if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 16) != hipSuccess)
+        return -1;
+    if (reset) {
+        unsigned long long z[16] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof z) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif
 
 extern "C" const char* qpsk_strerror(int err) {
     switch (err) {
