@@ -33,6 +33,29 @@ VALU_PEAK_TOPS = 78.6               # fp32 non-FMA lane-ops/s: 256 CU x 128 lane
 OPS_PER_SAMPLE_MIN = 96.0           # minimal bit-exact formulation
 
 
+def shard(channels: int, world: int, rank: int, strong: bool):
+    """(channels on this rank, first global channel id).  Weak: every rank
+    demodulates its own `channels`-channel batch (distinct channel ids); strong:
+    one `channels`-channel batch is split across the ranks."""
+    if strong:
+        base, rem = divmod(channels, world)
+        return base + (1 if rank < rem else 0), rank * base + min(rank, rem)
+    return channels, rank * channels
+
+
+def reduce_step(dist, wall: float, nch: int, device):
+    """Job time = MAX over ranks of the timed region; channels = SUM."""
+    import torch
+    if dist is None:
+        return wall, nch
+    t = torch.tensor([wall, float(nch)], dtype=torch.float64, device=device)
+    tmax = t[:1].clone()
+    dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    tot = t[1:].clone()
+    dist.all_reduce(tot)
+    return float(tmax.item()), int(tot.item())
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -64,12 +87,7 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
-    if args.strong:
-        base, rem = divmod(args.channels, world)
-        nch = base + (1 if rank < rem else 0)
-        c0 = rank * base + min(rank, rem)
-    else:
-        nch, c0 = args.channels, rank * args.channels
+    nch, c0 = shard(args.channels, world, rank, args.strong)
     nf = args.frames
 
     t = time.perf_counter()
@@ -105,16 +123,7 @@ def main():
     rx.timing(False)
     region_ms = ev0.elapsed_time(ev1)
 
-    tmax = wall
-    if dist:
-        tt = torch.tensor([wall], dtype=torch.float64, device=x.device)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        tmax = float(tt.item())
-        ntot = torch.tensor([nch], dtype=torch.float64, device=x.device)
-        dist.all_reduce(ntot)
-        total_ch = int(ntot.item())
-    else:
-        total_ch = nch
+    tmax, total_ch = reduce_step(dist, wall, nch, x.device)
     samples = float(total_ch) * nf * FRAME * args.steps
     value = samples / tmax / 1e6
 

@@ -86,3 +86,12 @@ def test_product_synth_matches_goldens(golden_dir):
         g = np.load(os.path.join(golden_dir, name + ".npz"))
         x = sc.synth(int(g["seed"]), int(g["nch"]), int(g["nframes"]), float(g["ebn0_db"]))
         assert hashlib.sha256(x.tobytes()).hexdigest() == str(g["input_sha256"])
+
+
+def test_c_driver_links_against_the_library():
+    """examples/qpsk_rx_raw.c: the reference RX loop relinked to libqpsk_hip.so."""
+    import subprocess
+    r = subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "examples")], capture_output=True,
+                       text=True)
+    assert r.returncode == 0, r.stderr
+    assert os.path.exists(os.path.join(ROOT, "examples", "qpsk_rx_raw"))
