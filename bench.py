@@ -66,7 +66,7 @@ def parse():
     ap.add_argument("--ebn0", type=float, default=1000.0, help=">= 100: noiseless")
     ap.add_argument("--seed", type=int, default=3)
     ap.add_argument("--strong", action="store_true", help="split --channels across ranks")
-    ap.add_argument("--cpu-channels", type=int, default=2048,
+    ap.add_argument("--cpu-channels", type=int, default=4096,
                     help="channels of the bounded CPU-baseline sample (0: skip)")
     ap.add_argument("--verify", type=int, default=256,
                     help="channels checked against the oracle after timing (0: skip)")
