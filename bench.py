@@ -70,11 +70,133 @@ def parse():
                     help="channels of the bounded CPU-baseline sample (0: skip)")
     ap.add_argument("--verify", type=int, default=256,
                     help="channels checked against the oracle after timing (0: skip)")
+    ap.add_argument("--sweep", action="store_true",
+                    help="C5: AWGN Eb/N0 sweep (GPU vs the reference C on host cores)")
+    ap.add_argument("--sweep-frames", type=int, default=16)
+    ap.add_argument("--sweep-points", type=str, default="0,1,2,3,4,5,6,7,8,9,10")
+    ap.add_argument("--cpu-procs", type=int, default=16)
     return ap.parse_args()
+
+
+# ----------------------------------------------------------------- C5 sweep
+_SM_K = 0x9E3779B97F4A7C15
+_M64 = (1 << 64) - 1
+
+
+def _sm64_next(s):
+    """splitmix64 over a uint64 numpy array (wrapping), as qpsk_synth.c."""
+    s = s + np.uint64(_SM_K)
+    z = s.copy()
+    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return s, z ^ (z >> np.uint64(31))
+
+
+def tx_frames(seed: int, c0: int, nch: int, nsamples: int):
+    """TX data-frame bits of every channel, regenerated from the generator's RNG
+    stream (include/qpsk_synth.h): uint64 [nch][nframes_tx] with bit 2s = Q,
+    bit 2s+1 = I of data symbol s (the reference's bits[] order)."""
+    with np.errstate(over="ignore"):
+        c = np.arange(c0, c0 + nch, dtype=np.uint64)
+        s = np.uint64(seed) ^ (c * np.uint64(_SM_K))
+        s, z = _sm64_next(s)
+        delay = (z % np.uint64(2783)).astype(np.int64)
+        npk = int(np.max((nsamples - delay + 2782) // 2783)) + 1
+        frames = np.zeros((nch, npk * 8), np.uint64)
+        for f in range(npk * 8):
+            w = np.zeros(nch, np.uint64)
+            for i in range(31):
+                s, z = _sm64_next(s)
+                dib = z & np.uint64(3)
+                w |= (dib & np.uint64(1)) << np.uint64(2 * i)           # Q
+                w |= (dib >> np.uint64(1)) << np.uint64(2 * i + 1)      # I
+            frames[:, f] = w
+    return frames
+
+
+def _pack62(bits):
+    w = np.zeros(bits.shape[:-1], np.uint64)
+    for k in range(62):
+        w |= bits[..., k].astype(np.uint64) << np.uint64(k)
+    return w
+
+
+def _ref_chunk(args):
+    import oracle
+    x, = args
+    b, v, _ = oracle.ref_rx(x)
+    return b, v
+
+
+def sweep(args):
+    """C5 (BASELINE.json configs[4]): AWGN Eb/N0 sweep over the channel batch.
+    Per point: GPU demod vs the unmodified reference C receiver on host cores
+    (disagreements must be 0) and BER against the transmitted bits, taken as
+    each valid frame's best match over that channel's TX data frames (the
+    reference modem does not recover TX data, SURVEY.md 0.6: BER ~ chance)."""
+    import multiprocessing as mp
+    import oracle
+    ctx = mp.get_context("spawn")
+    pool = ctx.Pool(args.cpu_procs)   # before any GPU use
+    import torch  # noqa: F401
+    import singlecarrier_amd as sc
+    nch, nf = args.channels, args.sweep_frames
+    ks = oracle.keystream(32767 + 62 * nf + 64)
+    ksw = np.array([int("".join(map(str, ks[62 * n:62 * n + 62][::-1])), 2) for n in range(nf)],
+                   np.uint64)
+    rows = []
+    for eb in [float(v) for v in args.sweep_points.split(",")]:
+        t0 = time.perf_counter()
+        x = sc.synth(args.seed, nch, nf, eb, threads=16)
+        t_syn = time.perf_counter() - t0
+        rx = sc.Receiver(nch)
+        t0 = time.perf_counter()
+        out = rx.demod(x)
+        t_gpu = time.perf_counter() - t0
+        rx.close()
+        chunks = np.array_split(np.arange(nch), args.cpu_procs * 4)
+        t0 = time.perf_counter()
+        res = pool.map(_ref_chunk, [(np.ascontiguousarray(x[c]),) for c in chunks])
+        t_cpu = time.perf_counter() - t0
+        rbits = np.concatenate([r[0] for r in res])
+        rvalid = np.concatenate([r[1] for r in res])
+        dis_bits = int((out["bits"] != rbits).sum())
+        dis_valid = int((out["valid"] != rvalid).sum())
+        tx = tx_frames(args.seed, 0, nch, nf * FRAME)
+        vm = out["valid"].astype(bool)
+        w = _pack62(out["bits"])
+        raw = w ^ ksw[None, :]            # before descrambling
+        best = np.full(w.shape, 62, np.int64)
+        best_raw = np.full(w.shape, 62, np.int64)
+        best_ctl = np.full(w.shape, 62, np.int64)      # control: another channel's TX
+        txo = np.roll(tx, 1, axis=0)
+        for f in range(tx.shape[1]):
+            best = np.minimum(best, np.bitwise_count(w ^ tx[:, f:f + 1]).astype(np.int64))
+            best_raw = np.minimum(best_raw, np.bitwise_count(raw ^ tx[:, f:f + 1]).astype(np.int64))
+            best_ctl = np.minimum(best_ctl, np.bitwise_count(w ^ txo[:, f:f + 1]).astype(np.int64))
+        nvalid = int(vm.sum())
+        row = {"ebn0_db": eb, "frames": int(nch * nf), "valid_frames": nvalid,
+               "valid_frac": round(nvalid / (nch * nf), 4),
+               "disagree_bits_vs_ref": dis_bits, "disagree_valid_vs_ref": dis_valid,
+               "ber_best_tx_match": round(float(best[vm].mean()) / 62, 4) if nvalid else None,
+               "ber_best_tx_match_raw": round(float(best_raw[vm].mean()) / 62, 4) if nvalid else None,
+               "ber_control_other_channel": round(float(best_ctl[vm].mean()) / 62, 4) if nvalid else None,
+               "gpu_s_incl_h2d": round(t_gpu, 3), "ref_cpu_s": round(t_cpu, 2),
+               "ref_cpu_msamples_s": round(nch * nf * FRAME / t_cpu / 1e6, 1),
+               "cpu_procs": args.cpu_procs, "synth_s": round(t_syn, 1)}
+        rows.append(row)
+        print(json.dumps(row), flush=True)
+    pool.close()
+    print(json.dumps({"sweep": "C5 AWGN Eb/N0", "channels": nch, "frames": nf,
+                      "all_identical_to_reference": all(r["disagree_bits_vs_ref"] == 0 and
+                                                       r["disagree_valid_vs_ref"] == 0
+                                                       for r in rows)}), flush=True)
 
 
 def main():
     args = parse()
+    if args.sweep:
+        return sweep(args)
     import torch
     import singlecarrier_amd as sc
 
