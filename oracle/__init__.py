@@ -197,3 +197,15 @@ def keystream(n: int) -> np.ndarray:
     ks = np.zeros(n, np.uint8)
     cpu_lib().qc_keystream(_p(ks), n)
     return ks
+
+
+def preamble() -> np.ndarray:
+    """The PN preamble p_i = +-1 (src/constants.c:25-42), read from the
+    restatement's own table in cpu_ref.c (k_pre)."""
+    import re
+    src = open(os.path.join(HERE, "cpu_ref.c")).read()
+    body = src[src.index("k_pre[QC_PRE] = {"):]
+    body = body[body.index("{") + 1:body.index("}")]
+    vals = [int(v) for v in re.findall(r"-?\d+", body)]
+    assert len(vals) == 128 and set(vals) == {-1, 1}
+    return np.asarray(vals, np.int8)

@@ -1,0 +1,21 @@
+#!/bin/bash
+# Kernel time of the full path and of each role alone (QPSK_ABLATE), plus SQ
+# instruction counters; one rocprofv3 pass each (run on the GPU box from the
+# repo root).   bash profiles/ablate.sh TAG [extra bench args]
+set -euo pipefail
+TAG=${1:-run}; shift || true
+OUT=gpurun_out/prof_$TAG
+mkdir -p $OUT
+export TMPDIR=/tmp
+B="bench.py --steps 2 --warmup 1 --cpu-channels 0 --verify 0 $*"
+run() { # name, rocprof args...
+  local name=$1; shift
+  timeout -k 10 300 rocprofv3 "$@" --output-format csv -d $OUT/$name -o $name -- python3 $B \
+    > $OUT/$name.log 2>&1
+}
+run stats --kernel-trace --stats
+run sq --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_LDS
+run mfma --kernel-trace --pmc SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_SALU
+export QPSK_ABLATE=back; run abl_back --kernel-trace --stats
+export QPSK_ABLATE=front; run abl_front --kernel-trace --stats; unset QPSK_ABLATE
+echo done > $OUT/DONE

@@ -28,6 +28,7 @@
 
 #include "qpsk_batch.h"
 #include "qpsk_consts.h"
+#include "qpsk_hunt.h"
 #include "qpsk_rcp.h"
 
 #pragma clang fp contract(off)
@@ -53,13 +54,7 @@ constexpr int kItems = kM / 2;         // 696 two-sample (dword) input items
 // fusion), and the halves never need repacking.
 typedef float f2 __attribute__((ext_vector_type(2)));
 
-constexpr unsigned long long pre_mask(int half) {
-    unsigned long long m = 0;
-    for (int i = 0; i < 64; i++)
-        if (QK_PRE[half * 64 + i] > 0) m |= 1ull << i;
-    return m;
-}
-constexpr unsigned long long kPreLo = pre_mask(0), kPreHi = pre_mask(1);
+constexpr unsigned long long kPreLo = qhunt::pre_mask(0), kPreHi = qhunt::pre_mask(1);
 
 struct RxArgs {
     const int16_t* in;       // [nch][F][1880]
@@ -222,7 +217,8 @@ __device__ __forceinline__ f2 ld2nt(const float2* p) {
 #define FACC_PARAM
 #define FACC_ARG
 #endif
-__device__ __forceinline__ int front_channel(int lane, int rt, float2* M, float2* dec FACC_PARAM) {
+__device__ __forceinline__ int front_channel(int lane, int rt, float2* M, float2* dec,
+                                             const float* BT FACC_PARAM) {
 #ifdef QPSK_STAMPS
     unsigned long long ft0 = stamp_now();
 #endif
@@ -283,58 +279,30 @@ __device__ __forceinline__ int front_channel(int lane, int rt, float2* M, float2
     }
     wave_lds_sync();
     FSTAMP(1);
-    // p*(dr-di, di+dr) == preambletable[i]*dec[j] exactly (p = +-1); TU reuses M.
-    float2* TU = M;
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-        const int j = lane + 64 * r;
-        if (j < 255) {
-            const float2 d = dec[j];
-            TU[j] = make_float2(d.x - d.y, d.y + d.x);
-        }
-    }
+    // correlate (src/qpsk.c:88-96) for all 128 lags on the matrix cores
+    // (qpsk_hunt.h: bit-identical k-ordered chain); the TK image reuses M.
+    float* TK = reinterpret_cast<float*>(M);
+    qhunt::store_t(lane, dec, TK);
     wave_lds_sync();
-    // correlate lags 2*lane and 2*lane+1 (src/qpsk.c:88-96), terms in index
-    // order; acc = acc +- (T, U) is one packed add
     FSTAMP(2);
-    f2 acc0 = {0.0f, 0.0f}, acc1 = {0.0f, 0.0f};
-    // lane l needs TU[2l + s], s = 0..128: pairs (s, s+1) with s even start at
-    // an even index, so each pair is one aligned, conflict-free ds_read_b128
-    const float4* tp = reinterpret_cast<const float4*>(TU + 2 * lane);
-#pragma unroll
-    for (int s0 = 0; s0 <= QK_NPRE; s0 += 16) {
-        f2 v[16];
-#pragma unroll
-        for (int j = 0; j < 16; j += 2) {
-            if (s0 + j <= QK_NPRE) {
-                const float4 q = tp[(s0 + j) >> 1];
-                v[j] = f2{q.x, q.y};
-                v[j + 1] = f2{q.z, q.w};
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < 16; j++) {
-            const int s = s0 + j;
-            if (s < QK_NPRE) acc0 = QK_PRE[s] > 0 ? acc0 + v[j] : acc0 - v[j];
-            if (s >= 1 && s <= QK_NPRE) acc1 = QK_PRE[s - 1] > 0 ? acc1 + v[j] : acc1 - v[j];
-        }
-    }
+    const qhunt::f4 acc = qhunt::correlate_bt(lane, TK, BT);
     FSTAMP(3);
-    const float r0 = acc0.x, i0 = acc0.y, r1 = acc1.x, i1 = acc1.y;
+    const float r0 = acc[0], i0 = acc[1], r1 = acc[2], i1 = acc[3];
     const float c0 = r0 * r0 + i0 * i0;    // cnormf, src/qpsk.c:75-80
     const float c1 = r1 * r1 + i1 * i1;
     // hunt (src/qpsk.c:172-183): first lag whose value is > the running max,
     // which starts at 0.  Values are >= 0 or NaN (never selected): map to
     // non-negative float bits (monotone as unsigned), take the wave max, then the
-    // lowest lag holding it; a maximum of 0 leaves max_index at 0.
+    // lowest lag holding it; a maximum of 0 leaves max_index at 0.  Lane order
+    // is lag order within each of the two fragments (qhunt::lag_lo/lag_hi).
     const unsigned k0 = c0 > 0.0f ? __float_as_uint(c0) : 0u;
     const unsigned k1 = c1 > 0.0f ? __float_as_uint(c1) : 0u;
     const unsigned km = wave_max_u32(max(k0, k1));
     FSTAMP(4);
     if (km == 0u) return 0;
     const unsigned long long m0 = __ballot(k0 == km), m1 = __ballot(k1 == km);
-    const int i0x = m0 ? 2 * (__ffsll((long long)m0) - 1) : 1 << 20;
-    const int i1x = m1 ? 2 * (__ffsll((long long)m1) - 1) + 1 : 1 << 20;
+    const int i0x = m0 ? qhunt::lag_lo(__ffsll((long long)m0) - 1) : 1 << 20;
+    const int i1x = m1 ? qhunt::lag_hi(__ffsll((long long)m1) - 1) : 1 << 20;
     return min(i0x, i1x);
 }
 
@@ -557,6 +525,7 @@ __global__ void __launch_bounds__(kBlock, 3) rx_kernel(
     __shared__ __attribute__((aligned(16))) float2 Ms[kFrontWaves][kM];
     __shared__ __attribute__((aligned(16))) float2 decs[kFrontWaves][2][kDec];
     __shared__ int mi_s[kGroups][2][QK_GROUP], rt_s[kGroups][2][QK_GROUP];
+    __shared__ __attribute__((aligned(16))) float BT[qhunt::kBT];   // correlator's B
     const int lane = threadIdx.x & 63;
     // wave-uniform by construction; readfirstlane tells the compiler, so every
     // per-wave index and pointer below lives in SGPRs
@@ -564,6 +533,7 @@ __global__ void __launch_bounds__(kBlock, 3) rx_kernel(
     const int grp0 = blockIdx.x * kGroups;
     for (int i = threadIdx.x; i < QK_FRAME / 2; i += kBlock)
         reinterpret_cast<float4*>(P)[i] = reinterpret_cast<const float4*>(a.ptab)[i];
+    qhunt::bconst_lds(threadIdx.x, kBlock, BT);
     if (wave < kGroups) {   // per-channel state of the groups at the call's first frame
         const int ch = (grp0 + wave) * QK_GROUP + lane;
         if (ch < a.nch) {
@@ -627,7 +597,7 @@ __global__ void __launch_bounds__(kBlock, 3) rx_kernel(
                 }
                 wave_lds_sync();
                 STAMP(1);
-                pmi = front_channel(lane, rt_s[gi][p][cbeg + c], M, dcur FACC_ARG);
+                pmi = front_channel(lane, rt_s[gi][p][cbeg + c], M, dcur, BT FACC_ARG);
                 if (lane == 0) mi_s[gi][p ^ 1][cbeg + c] = pmi;
                 if (c + 1 == nlive) store_window(lane, pmi, dcur, wout + (size_t)ch * kWinStride);
                 wave_lds_sync();
