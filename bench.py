@@ -241,7 +241,8 @@ def main():
     wall = time.perf_counter() - t0
     if dist:
         dist.barrier()
-    kern_ms, kern_frames = rx.collect_timing()
+    rx_ms, data_ms, kern_frames = rx.collect_timing_split()
+    kern_ms = rx_ms + data_ms
     rx.timing(False)
     region_ms = ev0.elapsed_time(ev1)
 
@@ -249,14 +250,18 @@ def main():
     samples = float(total_ch) * nf * FRAME * args.steps
     value = samples / tmax / 1e6
 
-    # roofline of the dominant kernel (rx_kernel: one persistent launch per step,
-    # all `frames` frames of all channels); duration from HIP events on its stream
+    # roofline of the path's kernels per step: rx_kernel (one persistent launch,
+    # all `frames` frames of all channels; dominant) + rx_data_kernel (data
+    # symbols of the valid frames).  Durations from HIP events on their stream;
+    # the algorithmic bytes of the step are divided by the SUM of both.
     t_launch = kern_ms / 1e3 / args.steps
     alg_bytes = nch * nf * ALG_BYTES_PER_FRAME
     achieved = alg_bytes / t_launch / 1e9
     roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-                "kernel": "rx_kernel", "launch_us": round(t_launch * 1e6, 2),
+                "kernel": "rx_kernel + rx_data_kernel", "launch_us": round(t_launch * 1e6, 2),
+                "kernels_us": {"rx_kernel": round(rx_ms / args.steps * 1e3, 2),
+                               "rx_data_kernel": round(data_ms / args.steps * 1e3, 2)},
                 "alg_bytes_per_launch": alg_bytes}
     pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc):

@@ -62,18 +62,21 @@ int qpsk_rx_batch(qpsk_ctx *ctx, const int16_t *in, int nframes, uint8_t *bits,
 
 /* Device-memory call: all pointers are device pointers on the context's device;
  * the work is enqueued on `stream` (a hipStream_t, NULL = default stream) and
- * the call returns without synchronising.  Launches one fused kernel per frame
- * plus one history update. */
+ * the call returns without synchronising.  Launches two kernels: rx_kernel
+ * (every stage of every frame, persistent over the call's frames) and
+ * rx_data_kernel (the 31 data symbols of the valid frames); see DESIGN.md. */
 int qpsk_rx_batch_device(qpsk_ctx *ctx, const int16_t *d_in, int nframes,
                          uint8_t *d_bits, uint8_t *d_valid, int32_t *d_trace,
                          float *d_soft, void *stream);
 
 /* Kernel-time accounting.  When enabled, every qpsk_rx_batch_device call
- * records a HIP event pair on its stream around its step-kernel launches (one
- * per frame); collect() waits for them and returns the summed span (ms) and the
- * number of step launches since the previous collect. */
+ * records HIP events on its stream before rx_kernel, between the two kernels
+ * and after rx_data_kernel.  collect() waits for them and returns the summed
+ * span of both kernels (ms) and the number of frames demodulated since the
+ * previous collect; split() returns the two kernels' spans separately. */
 int qpsk_rx_timing_enable(qpsk_ctx *ctx, int on);
-int qpsk_rx_timing_collect(qpsk_ctx *ctx, float *ms, int *launches);
+int qpsk_rx_timing_collect(qpsk_ctx *ctx, float *ms, int *frames);
+int qpsk_rx_timing_split(qpsk_ctx *ctx, float *ms_rx, float *ms_data, int *frames);
 
 /* Message for an error code (static storage). */
 const char *qpsk_strerror(int err);

@@ -78,6 +78,8 @@ def lib():
         L.qpsk_surface_error.restype = i32
         L.qpsk_rx_timing_enable.argtypes = [vp, i32]
         L.qpsk_rx_timing_collect.argtypes = [vp, C.POINTER(C.c_float), C.POINTER(C.c_int)]
+        L.qpsk_rx_timing_split.argtypes = [vp, C.POINTER(C.c_float), C.POINTER(C.c_float),
+                                           C.POINTER(C.c_int)]
         L.qpsk_synth_batch.restype = None
         L.qpsk_synth_batch.argtypes = [u64, C.c_uint32, i32, C.c_double, vp, C.c_long, i32]
         L.cnormf.restype = C.c_float
@@ -91,7 +93,7 @@ SYMBOLS = ["qpsk_rx_create", "qpsk_rx_destroy", "qpsk_rx_reset", "qpsk_rx_channe
            "cnormf", "qpsk_mod", "qpsk_demod", "qpsk_rx_frame", "qpsk_tx_frame",
            "qpsk_rx_init", "qpsk_tx_init", "qpsk_surface_error", "qpsk_tx_state_init",
            "qpsk_tx_frame_state", "qpsk_synth_batch", "qpsk_rx_timing_enable",
-           "qpsk_rx_timing_collect"]
+           "qpsk_rx_timing_collect", "qpsk_rx_timing_split"]
 
 
 def _check(rc: int) -> None:
@@ -141,10 +143,16 @@ class Receiver:
         _check(lib().qpsk_rx_timing_enable(self._h, int(on)))
 
     def collect_timing(self):
-        """(summed step-kernel span in ms, number of step launches) since last collect."""
+        """(summed kernel span in ms, frames) since the last collect."""
         ms, n = C.c_float(0), C.c_int(0)
         _check(lib().qpsk_rx_timing_collect(self._h, C.byref(ms), C.byref(n)))
         return float(ms.value), int(n.value)
+
+    def collect_timing_split(self):
+        """(rx_kernel ms, rx_data_kernel ms, frames) since the last collect."""
+        a, b, n = C.c_float(0), C.c_float(0), C.c_int(0)
+        _check(lib().qpsk_rx_timing_split(self._h, C.byref(a), C.byref(b), C.byref(n)))
+        return float(a.value), float(b.value), int(n.value)
 
     def demod(self, x, trace: bool = False, soft: bool = False):
         """Host arrays: x int16 [nch][nframes][1880] -> dict of numpy arrays

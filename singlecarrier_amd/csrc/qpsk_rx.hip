@@ -71,6 +71,8 @@ struct RxArgs {
     uint8_t* valid;          // [nch][F]
     int32_t* trace;          // [nch][F][4] or null
     float2* soft;            // [nch][F][31] or null
+    float4* jobs;            // data-symbol jobs of valid frames (rx_data_kernel)
+    unsigned* njobs;         // their count (this call's counter)
     int nch, F;
     unsigned g0;             // global index of the call's first frame
     int roles;               // bit 0: back, bit 1: front (3 in production); bits 4-5:
@@ -333,17 +335,30 @@ __device__ __forceinline__ f2 addsub(f2 a, f2 b) {
     asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1]" : "=v"(r) : "v"(a), "v"(b));
     return r;
 }
+// The two products, each ONE v_pk_mul_f32 with the broadcast/swap done by
+// op_sel (written out: LLVM otherwise copies the high half to a new register
+// before broadcasting it).
+__device__ __forceinline__ f2 mul_xx(f2 A, f2 C) {   // (A.x * C.x, A.x * C.y)
+    f2 r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(r) : "v"(A), "v"(C));
+    return r;
+}
+__device__ __forceinline__ f2 mul_yy_swap(f2 A, f2 C) {   // (A.y * C.y, A.y * C.x)
+    f2 r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[1,0]" : "=v"(r) : "v"(A), "v"(C));
+    return r;
+}
 __device__ __forceinline__ f2 cmul(f2 A, f2 C) {
-    const f2 t1 = A.xx * C;       // (ac, ad)
-    const f2 t2 = A.yy * C.yx;    // (bd, bc)
-    return addsub(t1, t2);        // (ac - bd, ad + bc)
+    const f2 t1 = mul_xx(A, C);        // (ac, ad)
+    const f2 t2 = mul_yy_swap(A, C);   // (bd, bc)
+    return addsub(t1, t2);             // (ac - bd, ad + bc)
 }
 // A * conj(C) as the reference rounds it: (a*c - b*(-d), a*(-d) + b*c).  Since
 // b*(-d) == -(b*d) and a*(-d) == -(a*d) exactly, that is (ac + bd, -(ad) + bc):
 // the same two packed products and ONE packed add with the high half of t1 negated.
 __device__ __forceinline__ f2 cmulc(f2 A, f2 C) {
-    const f2 t1 = A.xx * C;       // (ac, ad)
-    const f2 t2 = A.yy * C.yx;    // (bd, bc)
+    const f2 t1 = mul_xx(A, C);        // (ac, ad)
+    const f2 t2 = mul_yy_swap(A, C);   // (bd, bc)
     f2 r;
     asm("v_pk_add_f32 %0, %1, %2 neg_hi:[1,0]" : "=v"(r) : "v"(t1), "v"(t2));
     return r;
@@ -388,14 +403,15 @@ __device__ __forceinline__ void update_eq(Kal& k, const f2 (&x)[5], f2 e) {
     }
     const float hq = 1.0f + q;                            // 6.7
     const float ht = a[4] * q;
-    // the five divisor operands of 6.19 / 6.22; one range check for all of
-    // them (qk_rcp_fast == 1.0f / x inside it, see qpsk_rcp.h)
+    // the five divisor operands of 6.19 / 6.22.  They are nondecreasing in j:
+    // a_j = a_{j-1} + (gr*fr + gi*fi) and every g*conj(f) term is >= 0 (g = f*d,
+    // d > 0), so xs[0] >= E = 0.1 and xs[4] is the largest; one check of xs[4]
+    // (false for +inf/NaN, which propagate into a_4) covers all five
+    // (qk_rcp_fast == 1.0f / x inside [2^-125, 2^125], see qpsk_rcp.h).
     float xs[5], ys[5];
 #pragma unroll
     for (int j = 0; j < 5; j++) xs[j] = a[j] + ht;
-    const float lo = fminf(fminf(fminf(xs[0], xs[1]), fminf(xs[2], xs[3])), xs[4]);
-    const float hi = fmaxf(fmaxf(fmaxf(xs[0], xs[1]), fmaxf(xs[2], xs[3])), xs[4]);
-    if (__builtin_expect(qk_rcp_in_range(lo, hi), 1)) {
+    if (__builtin_expect(qk_rcp_in_range(xs[0], xs[4]), 1)) {
 #pragma unroll
         for (int j = 0; j < 5; j++) ys[j] = qk_rcp_fast(xs[j]);
     } else {
@@ -420,6 +436,56 @@ __device__ __forceinline__ void update_eq(Kal& k, const f2 (&x)[5], f2 e) {
     e = e * y;                                            // error *= kalman_y
 #pragma unroll
     for (int i = 0; i < 5; i++) k.eq[i] = k.eq[i] + cmulc(e, k.g[i]);
+}
+
+// A valid frame handed from the back wave to rx_data_kernel: the window
+// samples of its data symbols, the equalizer state after the 128 training
+// steps, and where its outputs go.  112 floats (28 x 16 B):
+//   [0, 70)  x = dec[mi+128+t], t < 35, as (re, im)
+//   [70, 80) eq[5]   [80, 100) u[10]   [100, 105) d[5] (one copy of each)
+//   [105, 107) cf (channel-frame index, 64-bit)   [107] keystream frame index
+constexpr int kJobF4 = 28;
+struct DataJob {
+    Kal k;
+    size_t cf;
+    unsigned ks;
+};
+
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+__device__ __forceinline__ void put_job(float4* out, const DataJob& j, const f2* x35) {
+    float v[112];
+#pragma unroll
+    for (int t = 0; t < 35; t++) { v[2 * t] = x35[t].x; v[2 * t + 1] = x35[t].y; }
+#pragma unroll
+    for (int t = 0; t < 5; t++) { v[70 + 2 * t] = j.k.eq[t].x; v[71 + 2 * t] = j.k.eq[t].y; }
+#pragma unroll
+    for (int t = 0; t < 10; t++) { v[80 + 2 * t] = j.k.u[t].x; v[81 + 2 * t] = j.k.u[t].y; }
+#pragma unroll
+    for (int t = 0; t < 5; t++) v[100 + t] = j.k.d[t].x;
+    v[105] = __uint_as_float((unsigned)(j.cf & 0xffffffffu));
+    v[106] = __uint_as_float((unsigned)(j.cf >> 32));
+    v[107] = __uint_as_float(j.ks);
+    v[108] = v[109] = v[110] = v[111] = 0.0f;
+#pragma unroll
+    for (int q = 0; q < kJobF4; q++) out[q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+}
+
+__device__ __forceinline__ void get_job(const float4* in, DataJob& j) {
+    float v[112];
+#pragma unroll
+    for (int q = 17; q < kJobF4; q++) {   // floats 68..111 (state and indices)
+        const float4 w = in[q];
+        v[4 * q] = w.x; v[4 * q + 1] = w.y; v[4 * q + 2] = w.z; v[4 * q + 3] = w.w;
+    }
+#pragma unroll
+    for (int t = 0; t < 5; t++) j.k.eq[t] = f2{v[70 + 2 * t], v[71 + 2 * t]};
+#pragma unroll
+    for (int t = 0; t < 10; t++) j.k.u[t] = f2{v[80 + 2 * t], v[81 + 2 * t]};
+#pragma unroll
+    for (int t = 0; t < 5; t++) { j.k.d[t] = f2{v[100 + t], v[100 + t]}; j.k.g[t] = f2{0.0f, 0.0f}; }
+    j.cf = (size_t)__float_as_uint(v[105]) | ((size_t)__float_as_uint(v[106]) << 32);
+    j.ks = __float_as_uint(v[107]);
 }
 
 // Window reads are plain loads: the window was stored by the front wave of this
@@ -453,6 +519,9 @@ __device__ __forceinline__ void back_frame(const RxArgs& a, int ch, bool live, i
     // equalize(): 128 x train_eq (src/qpsk.c:111-123, src/equalizer.c:45-58)
     const f2* wp2 = reinterpret_cast<const f2*>(win);
     int matches = 0;
+    // two steps per iteration: the allocator then alternates the registers of
+    // the loop-carried state instead of copying it back every step
+#pragma unroll 2
     for (int i = 0; i < QK_NPRE; i++) {
         const f2 nx = wp2[i + 6];                  // slot i+6 (next step)
         const unsigned long long m = i < 64 ? kPreLo : kPreHi;
@@ -469,37 +538,29 @@ __device__ __forceinline__ void back_frame(const RxArgs& a, int ch, bool live, i
     }
     const bool valid = live && matches > QK_MATCH_MIN;   // src/qpsk.c:196
     const size_t cf = (size_t)ch * a.F + n;
-    uint16_t* bo = reinterpret_cast<uint16_t*>(a.bits + cf * QK_NBITS);
-    float2* so = a.soft ? a.soft + cf * QK_NDSYM : nullptr;
-    const unsigned long long ks = a.ks[(a.g0 + (unsigned)n) % QK_KS_FRAMES];
-    // data symbols (src/qpsk.c:204-215): data_eq + qpsk_demod + scramble
-    for (int s = 0; s < QK_NDSYM; s += 2) {
-        float4 nx = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        if (valid) nx = ldw(wp + ((134 + s) >> 1));   // slots 134+s, 135+s
-#pragma unroll
-        for (int h = 0; h < 2; h++) {
-            const int ss = s + h;
-            if (ss < QK_NDSYM) {
-                uint16_t out = 0;
-                f2 sy = {0.0f, 0.0f};
-                if (valid) {
-#pragma unroll
-                    for (int t = 0; t < 5; t++) sy = sy + cmulc(x[t], k.eq[t]);
-                    const int dI = sy.x < 0.0f, dQ = sy.y < 0.0f;
-                    const f2 cst = {dI ? -1.0f : 1.0f, dQ ? -1.0f : 1.0f};
-                    update_eq(k, x, (cst - sy) * 0.1f);
-                    const int q = dQ ^ (int)((ks >> (2 * ss)) & 1ull);
-                    const int ib = dI ^ (int)((ks >> (2 * ss + 1)) & 1ull);
-                    out = (uint16_t)(q | (ib << 8));   // bits[2s] = Q, bits[2s+1] = I
-#pragma unroll
-                    for (int t = 0; t < 4; t++) x[t] = x[t + 1];
-                    x[4] = h ? f2{nx.z, nx.w} : f2{nx.x, nx.y};
-                }
-                if (live) {
-                    bo[ss] = out;
-                    if (so) so[ss] = make_float2(sy.x, sy.y);
-                }
-            }
+    // Valid frames continue in rx_data_kernel (data_eq needs nothing the next
+    // frame depends on): enqueue the equalizer state and the 35 window samples
+    // of the data symbols.  One slot reservation per wave.
+    const unsigned long long vm = __ballot(valid);
+    if (vm) {
+        unsigned base = 0;
+        if (lane_id() == 0) base = atomicAdd(a.njobs, (unsigned)__popcll(vm));
+        base = __builtin_amdgcn_readfirstlane(base);
+        if (valid) {
+            const unsigned slot = base + (unsigned)__popcll(vm & ((1ull << lane_id()) - 1ull));
+            DataJob j;
+            j.k = k;
+            j.cf = cf;
+            j.ks = (a.g0 + (unsigned)n) % QK_KS_FRAMES;
+            put_job(a.jobs + (size_t)slot * kJobF4, j, wp2 + 129);
+        }
+    }
+    if (live && !valid) {   // invalid frame: bits (and soft symbols) are zero
+        uint16_t* bo = reinterpret_cast<uint16_t*>(a.bits + cf * QK_NBITS);
+        for (int ss = 0; ss < QK_NDSYM; ss++) bo[ss] = 0;
+        if (a.soft) {
+            float2* so = a.soft + cf * QK_NDSYM;
+            for (int ss = 0; ss < QK_NDSYM; ss++) so[ss] = make_float2(0.0f, 0.0f);
         }
     }
     const int rtn = valid ? mi + QK_NPRE : rt;    // src/qpsk.c:219
@@ -511,6 +572,57 @@ __device__ __forceinline__ void back_frame(const RxArgs& a, int ch, bool live, i
     }
 }
 
+// ---------------------------------------------------------------- data kernel
+// The 31 data symbols of every valid frame (src/qpsk.c:204-215: data_eq
+// src/equalizer.c:64-90, qpsk_demod src/qpsk.c:268-271, scramble
+// src/scramble.c:57-84), one job per lane, packed: only ~1 frame in 5 is
+// valid, so running them inside the lane-per-channel back wave would idle most
+// lanes for 31 of its 159 steps.  Jobs come from the call's rx_kernel in any
+// order; every output location is fixed by the job, so results do not depend
+// on it.
+__global__ void __launch_bounds__(256) rx_data_kernel(const float4* jobs, unsigned* njobs,
+                                                      const unsigned long long* ks_tab,
+                                                      uint8_t* bits, float2* soft, int parity) {
+    const unsigned n = njobs[parity];
+    const unsigned stride = gridDim.x * blockDim.x;
+    for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const float4* jp = jobs + (size_t)i * kJobF4;
+        DataJob j;
+        get_job(jp, j);
+        const f2* xs = reinterpret_cast<const f2*>(jp);   // x = dec[mi+128+t], t < 35
+        f2 x[5];
+#pragma unroll
+        for (int t = 0; t < 5; t++) x[t] = xs[t];
+        const unsigned long long ks = ks_tab[j.ks];
+        float2* so = soft ? soft + j.cf * QK_NDSYM : nullptr;
+        Kal& k = j.k;
+        // decisions collect in a register; the 62 bytes are stored after the
+        // loop, so no wait on a store ever sits inside it
+        unsigned long long dib = 0;
+        for (int s = 0; s < QK_NDSYM; s++) {
+            const f2 nx = xs[min(s + 5, 34)];
+            f2 sy = {0.0f, 0.0f};
+#pragma unroll
+            for (int t = 0; t < 5; t++) sy = sy + cmulc(x[t], k.eq[t]);
+            const int dI = sy.x < 0.0f, dQ = sy.y < 0.0f;
+            const f2 cst = {dI ? -1.0f : 1.0f, dQ ? -1.0f : 1.0f};
+            update_eq(k, x, (cst - sy) * 0.1f);
+            dib |= (unsigned long long)(dQ | (dI << 1)) << (2 * s);   // bit 2s = Q, 2s+1 = I
+            if (so) so[s] = make_float2(sy.x, sy.y);
+#pragma unroll
+            for (int t = 0; t < 4; t++) x[t] = x[t + 1];
+            x[4] = nx;
+        }
+        dib ^= ks;   // descramble (src/scramble.c:57-84): keystream bits 62g .. 62g+61
+        uint16_t* bo = reinterpret_cast<uint16_t*>(bits + j.cf * QK_NBITS);
+#pragma unroll
+        for (int q = 0; q < QK_NDSYM; q++)
+            bo[q] = (uint16_t)(((dib >> (2 * q)) & 1ull) | (((dib >> (2 * q + 1)) & 1ull) << 8));
+    }
+    // the next call's counter (calls on one context are stream-ordered)
+    if (blockIdx.x == 0 && threadIdx.x == 0) njobs[parity ^ 1] = 0u;
+}
+
 // Plain pointer parameters (not a by-value struct): the compiler then knows every
 // pointer is a global-memory pointer (global_load/store, no flat) and nothing of
 // the argument block is indexed dynamically (no scratch copy).
@@ -518,9 +630,10 @@ __device__ __forceinline__ void back_frame(const RxArgs& a, int ch, bool live, i
 __global__ void __launch_bounds__(kBlock, 3) rx_kernel(
     const int16_t* in, int16_t* hist, const float2* ptab, const unsigned long long* ks,
     float2* win0, float2* win1, int* mi0, int* mi1, int* rt0, int* rt1, uint8_t* bits,
-    uint8_t* valid, int32_t* trace, float2* soft, int nch, int F, unsigned g0, int roles) {
+    uint8_t* valid, int32_t* trace, float2* soft, float4* jobs, unsigned* njobs, int nch, int F,
+    unsigned g0, int roles) {
     const RxArgs a{in, hist, ptab, ks, win0, win1, mi0, mi1, rt0, rt1, bits, valid, trace, soft,
-                   nch, F, g0, roles};
+                   jobs, njobs, nch, F, g0, roles};
     __shared__ __attribute__((aligned(16))) float2 P[QK_FRAME];
     __shared__ __attribute__((aligned(16))) float2 Ms[kFrontWaves][kM];
     __shared__ __attribute__((aligned(16))) float2 decs[kFrontWaves][2][kDec];
@@ -647,6 +760,11 @@ struct qpsk_ctx {
     float2* d_win[2] = {nullptr, nullptr};
     int* d_mi[2] = {nullptr, nullptr};
     int* d_rt[2] = {nullptr, nullptr};
+    // data-symbol jobs of valid frames (rx_kernel -> rx_data_kernel)
+    float4* d_jobs = nullptr;
+    size_t jobs_cap = 0;           // jobs (one per channel-frame of the largest call)
+    unsigned* d_njobs = nullptr;   // [2] counters, alternating by call
+    uint64_t calls = 0;
     // staging for the host-memory entry point
     int16_t* s_in = nullptr;
     uint8_t* s_bits = nullptr;
@@ -654,18 +772,19 @@ struct qpsk_ctx {
     int32_t* s_trace = nullptr;
     float* s_soft = nullptr;
     size_t s_frames = 0;
-    // kernel-span accounting: events around each call's kernel
+    // kernel-span accounting: events before rx_kernel, between the kernels, after
+    // rx_data_kernel
     static constexpr int kEv = 64;
-    hipEvent_t ev[kEv][2] = {};
+    hipEvent_t ev[kEv][3] = {};
     int ev_frames[kEv] = {};
     int ev_n = 0;
     bool timing = false;
     int roles = 3 | (1 << 4);   // roles + priority; QPSK_ABLATE / QPSK_PRIO (profiling)
-    float pend_ms = 0.0f;
+    float pend_ms[2] = {0.0f, 0.0f};
     int pend_frames = 0;
 };
 
-extern "C" int qpsk_rx_timing_collect(qpsk_ctx* c, float* ms, int* launches);
+extern "C" int qpsk_rx_timing_split(qpsk_ctx* c, float* ms_rx, float* ms_data, int* frames);
 
 static int herr(hipError_t e) { return e == hipSuccess ? QPSK_OK : QPSK_EHIP - (int)e; }
 #define HCHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) return herr(e_); } while (0)
@@ -706,6 +825,7 @@ static int ctx_alloc(qpsk_ctx* c) {
     HCHECK(hipMalloc(&c->d_ptab, sizeof(float2) * QK_FRAME));
     HCHECK(hipMalloc(&c->d_ks, sizeof(unsigned long long) * QK_KS_FRAMES));
     HCHECK(hipMalloc(&c->d_hist, sizeof(int16_t) * nslot(c) * 2 * QK_FRAME));
+    HCHECK(hipMalloc(&c->d_njobs, sizeof(unsigned) * 2));
     for (int p = 0; p < 2; p++) {
         HCHECK(hipMalloc(&c->d_win[p], sizeof(float2) * nslot(c) * kWinStride));
         HCHECK(hipMalloc(&c->d_mi[p], sizeof(int) * nslot(c)));
@@ -719,6 +839,7 @@ extern "C" int qpsk_rx_reset(qpsk_ctx* c) {
     HCHECK(hipSetDevice(c->device));
     const size_t ns = nslot(c);
     HCHECK(hipMemsetAsync(c->d_hist, 0, sizeof(int16_t) * ns * 2 * QK_FRAME, c->stream));
+    HCHECK(hipMemsetAsync(c->d_njobs, 0, sizeof(unsigned) * 2, c->stream));
     for (int p = 0; p < 2; p++) {
         HCHECK(hipMemsetAsync(c->d_win[p], 0, sizeof(float2) * ns * kWinStride, c->stream));
         HCHECK(hipMemsetAsync(c->d_mi[p], 0, sizeof(int) * ns, c->stream));
@@ -732,14 +853,17 @@ extern "C" int qpsk_rx_reset(qpsk_ctx* c) {
     HCHECK(e);
     HCHECK(hipStreamSynchronize(c->stream));
     c->frames = 0;
+    c->calls = 0;
     return QPSK_OK;
 }
 
 static void ctx_free(qpsk_ctx* c) {
     for (int i = 0; i < qpsk_ctx::kEv; i++)
-        for (int j = 0; j < 2; j++)
+        for (int j = 0; j < 3; j++)
             if (c->ev[i][j]) (void)hipEventDestroy(c->ev[i][j]);
     (void)hipFree(c->d_ptab);
+    (void)hipFree(c->d_jobs);
+    (void)hipFree(c->d_njobs);
     (void)hipFree(c->d_ks);
     (void)hipFree(c->d_hist);
     for (int p = 0; p < 2; p++) {
@@ -809,6 +933,9 @@ extern "C" void qpsk_rx_destroy(qpsk_ctx* c) {
 extern "C" int qpsk_rx_channels(const qpsk_ctx* c) { return c ? c->nch : 0; }
 extern "C" uint64_t qpsk_rx_frames(const qpsk_ctx* c) { return c ? c->frames : 0; }
 
+// rx_data_kernel grid: persistent, 4 workgroups of 256 per CU
+static constexpr int kDataBlocks = 1024, kDataThreads = 256;
+
 extern "C" int qpsk_rx_batch_device(qpsk_ctx* c, const int16_t* d_in, int F, uint8_t* d_bits,
                                     uint8_t* d_valid, int32_t* d_trace, float* d_soft,
                                     void* stream) {
@@ -817,31 +944,47 @@ extern "C" int qpsk_rx_batch_device(qpsk_ctx* c, const int16_t* d_in, int F, uin
     if ((reinterpret_cast<uintptr_t>(d_in) & 15u) != 0) return QPSK_EINVAL;  // int4 loads
     HCHECK(hipSetDevice(c->device));
     hipStream_t s = (hipStream_t)stream;
+    const size_t need = (size_t)c->nch * (size_t)F;   // every frame valid, at most
+    if (need > c->jobs_cap) {
+        HCHECK(hipDeviceSynchronize());   // an earlier call may still use the queue
+        (void)hipFree(c->d_jobs);
+        c->d_jobs = nullptr;
+        c->jobs_cap = 0;
+        HCHECK(hipMalloc(&c->d_jobs, sizeof(float4) * kJobF4 * need));
+        c->jobs_cap = need;
+    }
     int slot = -1;
     if (c->timing) {
         if (c->ev_n == qpsk_ctx::kEv) {   // pool full: fold pending spans into the totals
-            float ms;
+            float ms[2];
             int l;
-            int r = qpsk_rx_timing_collect(c, &ms, &l);
+            int r = qpsk_rx_timing_split(c, &ms[0], &ms[1], &l);
             if (r != QPSK_OK) return r;
-            c->pend_ms += ms;
+            c->pend_ms[0] += ms[0];
+            c->pend_ms[1] += ms[1];
             c->pend_frames += l;
         }
         slot = c->ev_n++;
-        for (int j = 0; j < 2; j++)
+        for (int j = 0; j < 3; j++)
             if (!c->ev[slot][j]) HCHECK(hipEventCreate(&c->ev[slot][j]));
         HCHECK(hipEventRecord(c->ev[slot][0], s));
         c->ev_frames[slot] = F;
     }
+    const int parity = (int)(c->calls & 1u);
     hipLaunchKernelGGL(rx_kernel, dim3((c->ngroup + kGroups - 1) / kGroups), dim3(kBlock), 0, s,
                        d_in, c->d_hist,
                        c->d_ptab, c->d_ks, c->d_win[0], c->d_win[1], c->d_mi[0], c->d_mi[1],
                        c->d_rt[0], c->d_rt[1], d_bits, d_valid, d_trace,
-                       reinterpret_cast<float2*>(d_soft), c->nch, F,
-                       (unsigned)(c->frames & 0xffffffffu), c->roles);
+                       reinterpret_cast<float2*>(d_soft), c->d_jobs, c->d_njobs + parity, c->nch,
+                       F, (unsigned)(c->frames & 0xffffffffu), c->roles);
     HCHECK(hipGetLastError());
     if (slot >= 0) HCHECK(hipEventRecord(c->ev[slot][1], s));
+    hipLaunchKernelGGL(rx_data_kernel, dim3(kDataBlocks), dim3(kDataThreads), 0, s, c->d_jobs,
+                       c->d_njobs, c->d_ks, d_bits, reinterpret_cast<float2*>(d_soft), parity);
+    HCHECK(hipGetLastError());
+    if (slot >= 0) HCHECK(hipEventRecord(c->ev[slot][2], s));
     c->frames += (uint64_t)F;
+    c->calls++;
     return QPSK_OK;
 }
 
@@ -851,24 +994,35 @@ extern "C" int qpsk_rx_timing_enable(qpsk_ctx* c, int on) {
     return QPSK_OK;
 }
 
-extern "C" int qpsk_rx_timing_collect(qpsk_ctx* c, float* ms, int* frames) {
-    if (!c || !ms || !frames) return QPSK_EINVAL;
+extern "C" int qpsk_rx_timing_split(qpsk_ctx* c, float* ms_rx, float* ms_data, int* frames) {
+    if (!c || !ms_rx || !ms_data || !frames) return QPSK_EINVAL;
     HCHECK(hipSetDevice(c->device));
-    float tot = c->pend_ms;
+    float tot[2] = {c->pend_ms[0], c->pend_ms[1]};
     int nf = c->pend_frames;
     for (int i = 0; i < c->ev_n; i++) {
-        HCHECK(hipEventSynchronize(c->ev[i][1]));
-        float t = 0.0f;
-        HCHECK(hipEventElapsedTime(&t, c->ev[i][0], c->ev[i][1]));
-        tot += t;
+        HCHECK(hipEventSynchronize(c->ev[i][2]));
+        for (int k = 0; k < 2; k++) {
+            float t = 0.0f;
+            HCHECK(hipEventElapsedTime(&t, c->ev[i][k], c->ev[i][k + 1]));
+            tot[k] += t;
+        }
         nf += c->ev_frames[i];
     }
     c->ev_n = 0;
-    c->pend_ms = 0.0f;
+    c->pend_ms[0] = c->pend_ms[1] = 0.0f;
     c->pend_frames = 0;
-    *ms = tot;
+    *ms_rx = tot[0];
+    *ms_data = tot[1];
     *frames = nf;
     return QPSK_OK;
+}
+
+extern "C" int qpsk_rx_timing_collect(qpsk_ctx* c, float* ms, int* frames) {
+    if (!ms) return QPSK_EINVAL;
+    float a = 0.0f, b = 0.0f;
+    const int r = qpsk_rx_timing_split(c, &a, &b, frames);
+    if (r == QPSK_OK) *ms = a + b;
+    return r;
 }
 
 static int stage_grow(qpsk_ctx* c, size_t F) {
