@@ -16,6 +16,7 @@ from collections import defaultdict
 
 d, tag, nch, nfr = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4])
 K = sys.argv[5] if len(sys.argv) > 5 else "rx_kernel"
+KD = "rx_data_kernel"
 
 
 def rows(pattern):
@@ -35,10 +36,11 @@ def short(name):
     return m.group(1) if m else name
 
 
-def counters(name):
+def counters(name, kern=None):
+    kern = kern or K
     acc = defaultdict(list)
     for x in rows(f"{name}/**/*counter_collection.csv"):
-        if K in x["Kernel_Name"]:
+        if short(x["Kernel_Name"]) == kern:
             acc[x["Counter_Name"]].append(float(x["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in acc.items()}
 
@@ -53,21 +55,25 @@ for ab in ("abl_back", "abl_front"):
     s = stats(ab)
     if K in s:
         lines.append(f"| {K} [{ab}: only the {ab[4:]} role runs] | {s[K][0]} | {s[K][1] / 1e3:.1f} |")
-c = {}
+c, cd = {}, {}
 for p in ("fetch", "write", "sq", "lds"):
     c.update(counters(p))
+    cd.update(counters(p, KD))
 t_ns = st[K][1]
-fetch_b = c.get("FETCH_SIZE", 0) * 1024 * 2   # KB, x2 gfx950 correction
-write_b = c.get("WRITE_SIZE", 0) * 1024
+t_dns = st[KD][1] if KD in st else 0.0
+# per step: rx_kernel + rx_data_kernel (the data symbols of the valid frames)
+fetch_b = (c.get("FETCH_SIZE", 0) + cd.get("FETCH_SIZE", 0)) * 1024 * 2   # KB, x2 gfx950 correction
+write_b = (c.get("WRITE_SIZE", 0) + cd.get("WRITE_SIZE", 0)) * 1024
 alg = nch * nfr * 3823
-lines += ["", f"## Counters per {K} dispatch (averages)", "", "| counter | value |", "|---|---|"]
+t_step = t_ns + t_dns
+lines += ["", f"## Counters per dispatch (averages)", "", f"| counter | {K} | {KD} |", "|---|---|---|"]
 for k in sorted(c):
-    lines.append(f"| {k} | {c[k]:.4g} |")
-lines += ["", "## Derived", "",
-          f"- HBM read bytes/launch (2 x FETCH_SIZE): {fetch_b / 1e6:.1f} MB; written (WRITE_SIZE): {write_b / 1e6:.1f} MB",
-          f"- algorithmic bytes/launch: {alg / 1e6:.1f} MB (3823 B per channel-frame, {nch} x {nfr})",
+    lines.append(f"| {k} | {c[k]:.4g} | {cd.get(k, float('nan')):.4g} |")
+lines += ["", "## Derived (per step = one rx_kernel + one rx_data_kernel launch)", "",
+          f"- HBM read bytes/step (2 x FETCH_SIZE): {fetch_b / 1e6:.1f} MB; written (WRITE_SIZE): {write_b / 1e6:.1f} MB",
+          f"- algorithmic bytes/step: {alg / 1e6:.1f} MB (3823 B per channel-frame, {nch} x {nfr})",
           f"- traffic / algorithmic = {(fetch_b + write_b) / alg:.2f}",
-          f"- achieved algorithmic GB/s = {alg / t_ns:.1f}; physical GB/s = {(fetch_b + write_b) / t_ns:.1f}"]
+          f"- kernel time/step: {t_ns / 1e3:.1f} + {t_dns / 1e3:.1f} us; achieved algorithmic GB/s = {alg / t_step:.1f}; physical GB/s = {(fetch_b + write_b) / t_step:.1f}"]
 if "SQ_WAVE_CYCLES" in c and "SQ_BUSY_CYCLES" in c:
     lines.append(f"- VALU instructions per wave-cycle: {c['SQ_INSTS_VALU'] / max(c['SQ_WAVE_CYCLES'], 1):.3f}; "
                  f"SQ_ACTIVE_INST_VALU/SQ_WAVE_CYCLES = {c['SQ_ACTIVE_INST_VALU'] / c['SQ_WAVE_CYCLES']:.3f}")
@@ -75,6 +81,7 @@ if "GRBM_GUI_ACTIVE" in c:
     lines.append(f"- effective clock ~ GRBM_GUI_ACTIVE/8/t = {c['GRBM_GUI_ACTIVE'] / 8 / t_ns:.2f} GHz")
 open(os.path.join("profiles", f"{tag}_summary.md"), "w").write("\n".join(lines) + "\n")
 json.dump({"channels": nch, "frames": nfr, "hbm_bytes_per_launch": int(fetch_b + write_b),
+           "kernels": [K, KD],
            "fetch_bytes": int(fetch_b), "write_bytes": int(write_b),
            "source": f"profiles/{tag}_summary.md (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes)"},
           open(os.path.join("profiles", "pmc_traffic.json"), "w"), indent=1)
