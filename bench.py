@@ -74,7 +74,10 @@ def parse():
                     help="C5: AWGN Eb/N0 sweep (GPU vs the reference C on host cores)")
     ap.add_argument("--sweep-frames", type=int, default=16)
     ap.add_argument("--sweep-points", type=str, default="0,1,2,3,4,5,6,7,8,9,10")
-    ap.add_argument("--cpu-procs", type=int, default=16)
+    ap.add_argument("--cpu-procs", type=int, default=16,
+                    help="host processes for the all-cores reference baseline and the sweep")
+    ap.add_argument("--cpu-all-channels", type=int, default=32768,
+                    help="channels of the all-cores reference sample (0: skip)")
     return ap.parse_args()
 
 
@@ -119,6 +122,18 @@ def _pack62(bits):
     for k in range(62):
         w |= bits[..., k].astype(np.uint64) << np.uint64(k)
     return w
+
+
+def _ref_timed(args):
+    """One host process of the all-cores baseline: regenerate its channels of
+    the benchmark workload (oracle.synth == the bench generator) and time the
+    unmodified reference over them, one channel after another."""
+    import oracle
+    seed, c0, n, nf, ebn0 = args
+    x = oracle.synth(seed, n, nf, ebn0, c0=c0, threads=1)
+    t = time.perf_counter()
+    oracle.ref_rx(x)
+    return n * nf * FRAME, time.perf_counter() - t
 
 
 def _ref_chunk(args):
@@ -197,10 +212,18 @@ def main():
     args = parse()
     if args.sweep:
         return sweep(args)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank0 = int(os.environ.get("RANK", "0")) == 0
+    pool = None
+    if rank0 and world == 1 and args.cpu_all_channels > 0 and args.cpu_procs > 1:
+        import multiprocessing as mp
+        import oracle
+        if oracle.ref_available():
+            pool = mp.get_context("spawn").Pool(args.cpu_procs)   # before any GPU use
+
     import torch
     import singlecarrier_amd as sc
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
@@ -308,6 +331,22 @@ def main():
                    "cores": 1, "kind": "port",
                    "sample": f"{k} channels x {nf} frames, oracle/cpu_ref.c, 1 thread, {dt:.1f} s"}
 
+    cpu_all = None
+    if pool is not None:
+        k = min(args.cpu_all_channels, nch)
+        bounds = np.linspace(0, k, args.cpu_procs + 1).astype(int)
+        jobs = [(args.seed, c0 + int(a), int(b - a), nf, args.ebn0)
+                for a, b in zip(bounds[:-1], bounds[1:]) if b > a]
+        res = pool.map(_ref_timed, jobs)
+        pool.close()
+        tot = sum(r[0] for r in res)
+        tmx = max(r[1] for r in res)
+        cpu_all = {"value": round(tot / tmx / 1e6, 3), "unit": "Msamples/s",
+                   "cores": len(jobs), "kind": "reference",
+                   "sample": f"{k} of the {nch} channels x {nf} frames, unmodified reference "
+                             f"(oracle/_ref, gcc -O2), {len(jobs)} host processes, "
+                             f"slowest {tmx:.1f} s"}
+
     if rank == 0:
         out = {
             "metric": METRIC, "value": round(value, 3), "unit": "Msamples/s",
@@ -323,6 +362,7 @@ def main():
                        "samples_per_step": int(total_ch * nf * FRAME),
                        "parallelism": f"channel shards x{world}, no collective"},
             "roofline": roofline, "valu": valu, "cpu_baseline": cpu,
+            "cpu_baseline_all_cores": cpu_all,
             "region_ms_per_step": round(region_ms / args.steps, 3),
             "synth_s": round(t_synth, 2), "h2d_s": round(t_h2d, 2),
             "h2d_incl_msamples_s": round(nch * nf * FRAME / (t_h2d + tmax / args.steps) / 1e6, 1),
