@@ -32,6 +32,18 @@ int qpsk_tx_frame_state(qpsk_tx_state *st, int16_t out[], const float *sym, int 
 void qpsk_synth_batch(uint64_t seed, uint32_t c0, int nch, double ebn0_db, int16_t *out,
                       long nsamples, int nthreads);
 
+/* The same streams generated on the GPU into device memory d_out [nch][nsamples]
+ * (current HIP device), enqueued on `stream` (hipStream_t, NULL = default).
+ * Noiseless output is identical to qpsk_synth_batch(); with noise the
+ * Box-Muller transcendentals are the device libm's (tests/test_gpu_synth.py
+ * compares).  Returns 0, -1 (bad argument), -2 (host allocation) or
+ * -1000 - hipError_t.  Blocks until the host-built phase table is uploaded. */
+int qpsk_synth_device(uint64_t seed, uint32_t c0, int nch, double ebn0_db, int16_t *d_out,
+                      long nsamples, void *stream);
+/* Carrier phase (re, im) of transmitted samples 0 .. ntx-1 of every channel
+ * (the transmitter's call sequence is the same for all channels). */
+void qpsk_tx_phase_table(float *out2, long ntx);
+
 #ifdef __cplusplus
 }
 #endif

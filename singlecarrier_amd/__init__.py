@@ -82,6 +82,9 @@ def lib():
                                            C.POINTER(C.c_int)]
         L.qpsk_synth_batch.restype = None
         L.qpsk_synth_batch.argtypes = [u64, C.c_uint32, i32, C.c_double, vp, C.c_long, i32]
+        L.qpsk_synth_device.argtypes = [u64, C.c_uint32, i32, C.c_double, vp, C.c_long, vp]
+        L.qpsk_tx_phase_table.restype = None
+        L.qpsk_tx_phase_table.argtypes = [vp, C.c_long]
         L.cnormf.restype = C.c_float
         L.cnormf.argtypes = [_CF]   # _Complex float == {float, float} in one SSE reg (SysV)
         _lib = L
@@ -93,7 +96,8 @@ SYMBOLS = ["qpsk_rx_create", "qpsk_rx_destroy", "qpsk_rx_reset", "qpsk_rx_channe
            "cnormf", "qpsk_mod", "qpsk_demod", "qpsk_rx_frame", "qpsk_tx_frame",
            "qpsk_rx_init", "qpsk_tx_init", "qpsk_surface_error", "qpsk_tx_state_init",
            "qpsk_tx_frame_state", "qpsk_synth_batch", "qpsk_rx_timing_enable",
-           "qpsk_rx_timing_collect", "qpsk_rx_timing_split"]
+           "qpsk_rx_timing_collect", "qpsk_rx_timing_split", "qpsk_synth_device",
+           "qpsk_tx_phase_table"]
 
 
 def _check(rc: int) -> None:
@@ -249,6 +253,28 @@ def synth(seed: int, nch: int, nframes: int, ebn0_db: float = 1000.0, c0: int = 
     threads = threads or min(16, os.cpu_count() or 1)
     lib().qpsk_synth_batch(seed, c0, nch, float(ebn0_db), _ptr(out), nframes * FRAME_SIZE,
                            threads)
+    return out
+
+
+def synth_device(seed: int, nch: int, nframes: int, ebn0_db: float = 1000.0, c0: int = 0,
+                 device: int | None = None, out=None):
+    """The same streams as synth(), generated on the GPU: a torch int16 tensor
+    [nch][nframes][1880] on `device` (qpsk_synth_device)."""
+    import torch
+    if out is None:
+        dev = torch.device("cuda", torch.cuda.current_device() if device is None else device)
+        out = torch.empty((nch, nframes, FRAME_SIZE), dtype=torch.int16, device=dev)
+    with torch.cuda.device(out.device):
+        stream = torch.cuda.current_stream().cuda_stream
+        _check(lib().qpsk_synth_device(seed, c0, nch, float(ebn0_db), out.data_ptr(),
+                                       nframes * FRAME_SIZE, stream))
+    return out
+
+
+def tx_phase_table(ntx: int) -> np.ndarray:
+    """Carrier phase of the first ntx transmitted samples, float32 [ntx][2]."""
+    out = np.empty((ntx, 2), np.float32)
+    lib().qpsk_tx_phase_table(_ptr(out), ntx)
     return out
 
 
