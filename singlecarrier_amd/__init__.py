@@ -85,6 +85,18 @@ def lib():
         L.qpsk_synth_device.argtypes = [u64, C.c_uint32, i32, C.c_double, vp, C.c_long, vp]
         L.qpsk_tx_phase_table.restype = None
         L.qpsk_tx_phase_table.argtypes = [vp, C.c_long]
+        L.qpsk_stream_create.restype = vp
+        L.qpsk_stream_create.argtypes = [i32, i32, i32, i32, C.POINTER(C.c_int)]
+        L.qpsk_stream_destroy.argtypes = [vp]
+        L.qpsk_stream_acquire.restype = vp
+        L.qpsk_stream_acquire.argtypes = [vp, C.POINTER(C.c_int)]
+        L.qpsk_stream_submit.argtypes = [vp]
+        L.qpsk_stream_pending.argtypes = [vp]
+        L.qpsk_stream_retrieve.argtypes = [vp, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]
+        L.qpsk_stream_ctx.restype = vp
+        L.qpsk_stream_ctx.argtypes = [vp]
+        L.qpsk_records.restype = C.c_size_t
+        L.qpsk_records.argtypes = [vp, vp, i32, vp]
         L.cnormf.restype = C.c_float
         L.cnormf.argtypes = [_CF]   # _Complex float == {float, float} in one SSE reg (SysV)
         _lib = L
@@ -97,7 +109,9 @@ SYMBOLS = ["qpsk_rx_create", "qpsk_rx_destroy", "qpsk_rx_reset", "qpsk_rx_channe
            "qpsk_rx_init", "qpsk_tx_init", "qpsk_surface_error", "qpsk_tx_state_init",
            "qpsk_tx_frame_state", "qpsk_synth_batch", "qpsk_rx_timing_enable",
            "qpsk_rx_timing_collect", "qpsk_rx_timing_split", "qpsk_synth_device",
-           "qpsk_tx_phase_table"]
+           "qpsk_tx_phase_table", "qpsk_stream_create", "qpsk_stream_destroy",
+           "qpsk_stream_acquire", "qpsk_stream_submit", "qpsk_stream_pending",
+           "qpsk_stream_retrieve", "qpsk_stream_ctx", "qpsk_records"]
 
 
 def _check(rc: int) -> None:
@@ -197,6 +211,54 @@ class Receiver:
 
 # --- the reference's single-channel surface (headers/qpsk_internal.h:79-84) ---
 
+class Stream:
+    """Streaming ingest over pinned chunk slots (include/qpsk_stream.h): fill
+    ``acquire()`` in place, ``submit()``, later ``retrieve()`` the oldest chunk.
+    Every channel's state carries across chunks."""
+
+    def __init__(self, nch: int, frames: int, nslot: int = 3, device: int = 0):
+        err = C.c_int(0)
+        self._h = lib().qpsk_stream_create(device, nch, frames, nslot, C.byref(err))
+        if not self._h:
+            _check(err.value or -3)
+        self.nch, self.frames, self.nslot = nch, frames, nslot
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            lib().qpsk_stream_destroy(self._h)
+            self._h = None
+
+    __del__ = close
+
+    def acquire(self) -> np.ndarray:
+        """The next chunk's pinned input buffer as int16 [nch][frames][1880]."""
+        err = C.c_int(0)
+        p = lib().qpsk_stream_acquire(self._h, C.byref(err))
+        if not p:
+            _check(err.value or -1)
+        n = self.nch * self.frames * FRAME_SIZE
+        buf = (C.c_int16 * n).from_address(p)
+        return np.frombuffer(buf, np.int16).reshape(self.nch, self.frames, FRAME_SIZE)
+
+    def submit(self) -> None:
+        _check(lib().qpsk_stream_submit(self._h))
+
+    @property
+    def pending(self) -> int:
+        return int(lib().qpsk_stream_pending(self._h))
+
+    def retrieve(self, copy: bool = True):
+        """(bits [nch][frames][62], valid [nch][frames]) of the oldest chunk."""
+        b, v = C.c_void_p(), C.c_void_p()
+        _check(lib().qpsk_stream_retrieve(self._h, C.byref(b), C.byref(v)))
+        cf = self.nch * self.frames
+        bits = np.frombuffer((C.c_uint8 * (cf * NBITS)).from_address(b.value), np.uint8)
+        valid = np.frombuffer((C.c_uint8 * cf).from_address(v.value), np.uint8)
+        bits = bits.reshape(self.nch, self.frames, NBITS)
+        valid = valid.reshape(self.nch, self.frames)
+        return (bits.copy(), valid.copy()) if copy else (bits, valid)
+
+
 def cnormf(val: complex) -> float:
     """|val|^2 as the reference computes it (src/qpsk.c:75-80)."""
     return float(lib().cnormf(_CF(val.real, val.imag)))
@@ -288,10 +350,11 @@ def read_raw(path: str) -> np.ndarray:
 
 def records(bits: np.ndarray, valid: np.ndarray) -> bytes:
     """The reference driver's output file (src/qpsk.c:455-457): one 496-byte
-    record per valid frame, bits in bytes 0..61, the rest zero."""
-    out = bytearray()
-    for n in np.flatnonzero(valid):
-        rec = np.zeros(BITS_PER_FRAME, np.uint8)
-        rec[:NBITS] = bits[n]
-        out += rec.tobytes()
-    return bytes(out)
+    record per valid frame, bits in bytes 0..61, the rest zero (qpsk_records,
+    host code)."""
+    bits = np.ascontiguousarray(bits, np.uint8)
+    valid = np.ascontiguousarray(valid, np.uint8)
+    nf = valid.shape[0]
+    out = np.empty(max(nf, 1) * BITS_PER_FRAME, np.uint8)
+    n = lib().qpsk_records(_ptr(bits), _ptr(valid), nf, _ptr(out))
+    return out[:n].tobytes()

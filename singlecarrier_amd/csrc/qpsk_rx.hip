@@ -1087,6 +1087,7 @@ extern "C" const char* qpsk_strerror(int err) {
         case QPSK_EINVAL: return "invalid argument";
         case QPSK_ENOMEM: return "out of memory";
         case QPSK_ENODEV: return "no such HIP device";
+        case -4: return "every stream slot is in flight (retrieve first)";
         default: break;
     }
     if (err <= QPSK_EHIP) return hipGetErrorString((hipError_t)(QPSK_EHIP - err));

@@ -14,7 +14,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def _declared():
     names = set()
-    for h in ("qpsk_internal.h", "qpsk_batch.h", "qpsk_synth.h"):
+    for h in sorted(os.listdir(os.path.join(ROOT, "include"))):
+        if not h.endswith(".h"):
+            continue
         src = open(os.path.join(ROOT, "include", h)).read()
         src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
         for m in re.finditer(r"\b([a-z_][a-z0-9_]*)\s*\(", src):
@@ -95,3 +97,22 @@ def test_c_driver_links_against_the_library():
                        text=True)
     assert r.returncode == 0, r.stderr
     assert os.path.exists(os.path.join(ROOT, "examples", "qpsk_rx_raw"))
+
+
+def test_record_writer_reproduces_reference_output_file(golden_dir):
+    """qpsk_records (include/qpsk_stream.h, host code): the reference driver's
+    496-byte records (src/qpsk.c:455-457) from the golden per-frame outputs of
+    preamble_qpsk_8k.raw give the reference output file (md5 b56a4d36...)."""
+    import hashlib
+    import json
+    exp = json.load(open(os.path.join(golden_dir, "sample_expected.json")))
+    nf = exp["frames"]
+    bits = np.zeros((nf, 62), np.uint8)
+    valid = np.zeros(nf, np.uint8)
+    for n, b in exp["valid_bits"].items():
+        valid[int(n)] = 1
+        bits[int(n)] = [int(ch) for ch in b]
+    recs = sc.records(bits, valid)
+    assert len(recs) == exp["output_bytes"] == 496 * int(valid.sum())
+    assert hashlib.md5(recs).hexdigest() == exp["output_md5"]
+    assert sc.records(bits, np.zeros(nf, np.uint8)) == b""
