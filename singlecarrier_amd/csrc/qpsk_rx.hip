@@ -163,30 +163,43 @@ __device__ __forceinline__ void prefetch(const Src& s, int lane, int (&r)[kPf]) 
     load_item<9>(s, lane, r[9]); load_item<10>(s, lane, r[10]);
 }
 
-// src/qpsk.c:139-144 as (-1)^G * P[t] * (x * 2^-14), two samples per item
-template <int i>
-__device__ __forceinline__ void mix_item(int lane, int r, bool neg_odd, bool neg_even,
-                                         const float2* P, float2* M) {
+// src/qpsk.c:139-144 as (-1)^G * P[t] * (x * 2^-14), two samples per item.
+// NO: frame g-1 (f == 1) is the negated one (then g-2 and g are not).  Items
+// 1..9 hold frame g-1 in every lane, so their sign is a compile-time negation
+// (a free source modifier); items 0 and 10 straddle two frames per lane.
+template <int i, bool NO>
+__device__ __forceinline__ void mix_item(int lane, int r, const float2* P, float2* M) {
     int t;
     const int f = item<i>(lane, t);
     if (f < 0) return;
     const float4 p = *reinterpret_cast<const float4*>(P + t);
-    const float sg = (f == 1 ? neg_odd : neg_even) ? -1.0f : 1.0f;   // exact sign flip
     const float v0 = (float)(int16_t)(r & 0xffff);
     const float v1 = (float)(int16_t)(r >> 16);
-    *reinterpret_cast<float4*>(M + 2 * (lane + 64 * i)) =
-        make_float4((sg * p.x) * v0, (sg * p.y) * v0, (sg * p.z) * v1, (sg * p.w) * v1);
+    float4 o;
+    if (i >= 1 && i <= 9) {
+        o = NO ? make_float4((-p.x) * v0, (-p.y) * v0, (-p.z) * v1, (-p.w) * v1)
+               : make_float4(p.x * v0, p.y * v0, p.z * v1, p.w * v1);
+    } else {
+        const float sg = ((f == 1) == NO) ? -1.0f : 1.0f;   // exact sign flip
+        o = make_float4((sg * p.x) * v0, (sg * p.y) * v0, (sg * p.z) * v1, (sg * p.w) * v1);
+    }
+    *reinterpret_cast<float4*>(M + 2 * (lane + 64 * i)) = o;
+}
+
+template <bool NO>
+__device__ __forceinline__ void mix_all(int lane, const int (&r)[kPf], const float2* P, float2* M) {
+    mix_item<0, NO>(lane, r[0], P, M); mix_item<1, NO>(lane, r[1], P, M);
+    mix_item<2, NO>(lane, r[2], P, M); mix_item<3, NO>(lane, r[3], P, M);
+    mix_item<4, NO>(lane, r[4], P, M); mix_item<5, NO>(lane, r[5], P, M);
+    mix_item<6, NO>(lane, r[6], P, M); mix_item<7, NO>(lane, r[7], P, M);
+    mix_item<8, NO>(lane, r[8], P, M); mix_item<9, NO>(lane, r[9], P, M);
+    mix_item<10, NO>(lane, r[10], P, M);
 }
 
 __device__ __forceinline__ void mix(int lane, const int (&r)[kPf], unsigned g, const float2* P,
                                     float2* M) {
-    const bool no = ((g - 1u) & 1u) != 0, ne = (g & 1u) != 0;   // frames g-1 | g, g-2
-    mix_item<0>(lane, r[0], no, ne, P, M); mix_item<1>(lane, r[1], no, ne, P, M);
-    mix_item<2>(lane, r[2], no, ne, P, M); mix_item<3>(lane, r[3], no, ne, P, M);
-    mix_item<4>(lane, r[4], no, ne, P, M); mix_item<5>(lane, r[5], no, ne, P, M);
-    mix_item<6>(lane, r[6], no, ne, P, M); mix_item<7>(lane, r[7], no, ne, P, M);
-    mix_item<8>(lane, r[8], no, ne, P, M); mix_item<9>(lane, r[9], no, ne, P, M);
-    mix_item<10>(lane, r[10], no, ne, P, M);
+    if (((g - 1u) & 1u) != 0) mix_all<true>(lane, r, P, M);   // frame g-1 odd
+    else mix_all<false>(lane, r, P, M);
 }
 
 // max over the 64 lanes of a wave (DPP row shifts / row broadcasts, no LDS trips)
