@@ -37,7 +37,8 @@ torch.cuda.synchronize()
 lib.qpsk_debug_stamps(st.ctypes.data, 1)
 names = {0: "mix", 1: "store_window+prefetch+sync", 6: "front_channel+mi+sync (total)",
          7: "frame barrier wait", 8: "FIR decimated (D)", 9: "FIR head (F)+sync",
-         10: "TU+sync", 11: "correlate", 12: "argmax (DPP max)"}
+         10: "T image+sync", 11: "correlate (MFMA)", 12: "argmax (DPP max)"}
+bnames = {13: "back: frame (128 train steps + job/outputs)", 14: "back: frame barrier wait"}
 ch_iters = nch * nf  # front-wave channel iterations (each wave does 32 per frame)
 waves = nch // 32
 out = {"mode": mode, "cycles_per_channel": {}}
@@ -46,4 +47,8 @@ for i, nm in names.items():
     v = int(st[i]) / ch_iters  # lane-0 sums: cycles per channel iteration
     out["cycles_per_channel"][nm] = round(v, 1)
 out["share_of_loop"] = {names[i]: round(int(st[i]) / tot, 3) for i in (0, 1, 6, 7)}
+bw = nch // 64   # back waves
+btot = int(st[13]) + int(st[14])
+out["back_cycles_per_frame"] = {bnames[i]: round(int(st[i]) / (bw * nf), 1) for i in (13, 14)}
+out["back_share"] = {bnames[i]: round(int(st[i]) / max(btot, 1), 3) for i in (13, 14)}
 print(json.dumps(out, indent=1))
