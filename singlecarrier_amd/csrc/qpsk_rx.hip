@@ -675,6 +675,7 @@ __global__ void __launch_bounds__(kBlock, 3) rx_kernel(
         const bool live = ch < a.nch;
         const bool any = (grp0 + gi) * QK_GROUP < a.nch;
         if (((a.roles >> 4) & 3) == 2) __builtin_amdgcn_s_setprio(2);
+        STAMP_DECL
         for (int n = 0; n < a.F; n++) {
             const int p = n & 1;
             if (any && (a.roles & 1))
@@ -683,8 +684,11 @@ __global__ void __launch_bounds__(kBlock, 3) rx_kernel(
                            &rt_s[gi][p ^ 1][lane]);
             else
                 rt_s[gi][p ^ 1][lane] = rt_s[gi][p][lane];
+            STAMP(13);
             __syncthreads();
+            STAMP(14);
         }
+        STAMP_FLUSH();
         if (live) {   // per-channel state after the call's last frame
             const unsigned ge = a.g0 + (unsigned)a.F;
             mi_of(a, ge)[ch] = mi_s[gi][a.F & 1][lane];
