@@ -35,13 +35,11 @@
 
 namespace {
 
-// A workgroup owns kGroups groups of 64 channels: waves 0..kGroups-1 are their
-// back waves, waves kGroups.. are front waves, kFrontPer per group.
-constexpr int kGroups = 4;
-constexpr int kFrontPer = 2;
-constexpr int kFrontCh = QK_GROUP / kFrontPer;     // 32 channels per front wave
-constexpr int kFrontWaves = kGroups * kFrontPer;
-constexpr int kBlock = 64 * (kGroups + kFrontWaves);   // 768 threads, 12 waves
+// A workgroup owns G groups of 64 channels: waves 0..G-1 are their back waves,
+// waves G.. are front waves, FP per group (rx_kernel<G, FP>).  Every shape has
+// 8 front waves, so the LDS footprint is the same; large batches use G = 4
+// (256 channels per CU), smaller ones spread over more CUs with G = 2 or 1.
+constexpr int kMaxGroups = 4;
 constexpr int kWinStride = 168;        // window row: slot k+1 = dec[mi+k], 84 float4
 // front LDS (float2 units): M = m_{n-2}[1832..1879] ++ m_{n-1}[0..1191]   (1240)
 //                            ++ m_{n-1}[1832..1879] ++ m_n[0..103]        (152)
@@ -640,11 +638,16 @@ __global__ void __launch_bounds__(256) rx_data_kernel(const float4* jobs, unsign
 // pointer is a global-memory pointer (global_load/store, no flat) and nothing of
 // the argument block is indexed dynamically (no scratch copy).
 // 12 waves per workgroup, 3 per SIMD (<= 168 VGPRs), one workgroup per CU (LDS).
-__global__ void __launch_bounds__(kBlock, 3) rx_kernel(
+template <int G, int FP>
+__global__ void __launch_bounds__(64 * G * (1 + FP), 3) rx_kernel(
     const int16_t* in, int16_t* hist, const float2* ptab, const unsigned long long* ks,
     float2* win0, float2* win1, int* mi0, int* mi1, int* rt0, int* rt1, uint8_t* bits,
     uint8_t* valid, int32_t* trace, float2* soft, float4* jobs, unsigned* njobs, int nch, int F,
     unsigned g0, int roles) {
+    constexpr int kGroups = G, kFrontPer = FP;
+    constexpr int kFrontCh = QK_GROUP / kFrontPer;     // channels per front wave
+    constexpr int kFrontWaves = kGroups * kFrontPer;
+    constexpr int kBlock = 64 * (kGroups + kFrontWaves);
     const RxArgs a{in, hist, ptab, ks, win0, win1, mi0, mi1, rt0, rt1, bits, valid, trace, soft,
                    jobs, njobs, nch, F, g0, roles};
     __shared__ __attribute__((aligned(16))) float2 P[QK_FRAME];
@@ -797,6 +800,8 @@ struct qpsk_ctx {
     int ev_n = 0;
     bool timing = false;
     int roles = 3 | (1 << 4);   // roles + priority; QPSK_ABLATE / QPSK_PRIO (profiling)
+    int ncu = 256;              // compute units of the device
+    int shape_groups = 0;       // 0: by batch size; QPSK_SHAPE (A/B experiments)
     float pend_ms[2] = {0.0f, 0.0f};
     int pend_frames = 0;
 };
@@ -833,9 +838,9 @@ static void build_tables(float2* ptab, unsigned long long* ksf) {
     }
 }
 
-// state arrays cover whole workgroups (kGroups groups of 64 channels)
+// state arrays cover whole workgroups of the largest shape (kMaxGroups groups)
 static size_t nslot(const qpsk_ctx* c) {
-    return (size_t)((c->ngroup + kGroups - 1) / kGroups) * kGroups * QK_GROUP;
+    return (size_t)((c->ngroup + kMaxGroups - 1) / kMaxGroups) * kMaxGroups * QK_GROUP;
 }
 
 static int ctx_alloc(qpsk_ctx* c) {
@@ -918,7 +923,15 @@ extern "C" qpsk_ctx* qpsk_rx_create(int device, int nch, int* err) {
         const int v = !strcmp(pr, "front") ? 1 : !strcmp(pr, "back") ? 2 : 0;
         c->roles = (c->roles & 3) | (v << 4);
     }
+    if (const char* sh = getenv("QPSK_SHAPE"))
+        c->shape_groups = !strcmp(sh, "1x8") ? 1 : !strcmp(sh, "2x4") ? 2 : !strcmp(sh, "4x2") ? 4 : 0;
     int r = herr(hipSetDevice(device));
+    if (r == QPSK_OK) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
+            n > 0)
+            c->ncu = n;
+    }
     if (r == QPSK_OK) r = herr(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     if (r == QPSK_OK) r = ctx_alloc(c);
     if (r == QPSK_OK) {
@@ -988,12 +1001,21 @@ extern "C" int qpsk_rx_batch_device(qpsk_ctx* c, const int16_t* d_in, int F, uin
         c->ev_frames[slot] = F;
     }
     const int parity = (int)(c->calls & 1u);
-    hipLaunchKernelGGL(rx_kernel, dim3((c->ngroup + kGroups - 1) / kGroups), dim3(kBlock), 0, s,
-                       d_in, c->d_hist,
-                       c->d_ptab, c->d_ks, c->d_win[0], c->d_win[1], c->d_mi[0], c->d_mi[1],
-                       c->d_rt[0], c->d_rt[1], d_bits, d_valid, d_trace,
-                       reinterpret_cast<float2*>(d_soft), c->d_jobs, c->d_njobs + parity, c->nch,
-                       F, (unsigned)(c->frames & 0xffffffffu), c->roles);
+    // workgroup shape: the fewest groups per workgroup that still fit the
+    // batch in one wave of workgroups (QPSK_SHAPE=4x2|2x4|1x8 overrides)
+    const int G = c->shape_groups > 0 ? c->shape_groups
+                : c->ngroup <= c->ncu ? 1 : c->ngroup <= 2 * c->ncu ? 2 : 4;
+#define QPSK_LAUNCH(GG, FF)                                                                    \
+    hipLaunchKernelGGL((rx_kernel<GG, FF>), dim3((c->ngroup + GG - 1) / GG),                  \
+                       dim3(64 * GG * (1 + FF)), 0, s, d_in, c->d_hist, c->d_ptab, c->d_ks,    \
+                       c->d_win[0], c->d_win[1], c->d_mi[0], c->d_mi[1], c->d_rt[0], c->d_rt[1], \
+                       d_bits, d_valid, d_trace, reinterpret_cast<float2*>(d_soft), c->d_jobs,  \
+                       c->d_njobs + parity, c->nch, F, (unsigned)(c->frames & 0xffffffffu),     \
+                       c->roles)
+    if (G == 1) QPSK_LAUNCH(1, 8);
+    else if (G == 2) QPSK_LAUNCH(2, 4);
+    else QPSK_LAUNCH(4, 2);
+#undef QPSK_LAUNCH
     HCHECK(hipGetLastError());
     if (slot >= 0) HCHECK(hipEventRecord(c->ev[slot][1], s));
     hipLaunchKernelGGL(rx_data_kernel, dim3(kDataBlocks), dim3(kDataThreads), 0, s, c->d_jobs,

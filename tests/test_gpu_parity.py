@@ -211,3 +211,12 @@ def test_c_driver_single_and_batch(golden_dir, tmp_path):
     bits, valid, _ = oracle.cpu_rx(syn)
     for i in range(2):
         assert (tmp_path / f"ch{i + 1}.bin").read_bytes() == sc.records(bits[i], valid[i])
+
+
+@pytest.mark.parametrize("shape", ["4x2", "2x4", "1x8"])
+def test_every_workgroup_shape(shape, monkeypatch):
+    """rx_kernel<G, FP> (groups per workgroup x front waves per group) is chosen
+    by batch size; QPSK_SHAPE forces each one on the same ragged batch."""
+    monkeypatch.setenv("QPSK_SHAPE", shape)
+    x = oracle.synth(61, 300, 12, 5.0)
+    _vs_oracle(x)
