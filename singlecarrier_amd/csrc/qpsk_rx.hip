@@ -392,7 +392,13 @@ struct Kal {
 __host__ __device__ constexpr int uix(int i, int j) { return j * (j - 1) / 2 + i; }
 
 // kalman_calculate (src/kalman.c:85-141) then update_eq (src/equalizer.c:25-40)
-__device__ __forceinline__ void update_eq(Kal& k, const f2 (&x)[5], f2 e) {
+// EXACT = false: the five divisions use the fast correctly-rounded reciprocal
+// (qpsk_rcp.h), valid inside [2^-125, 2^125]; `bad` collects lanes whose
+// operands left that range (never seen: they are >= 0.1), and the caller then
+// recomputes the whole frame with EXACT = true (IEEE division).  No branch in
+// the step, so the step is one basic block.
+template <bool EXACT>
+__device__ __forceinline__ void update_eq(Kal& k, const f2 (&x)[5], f2 e, bool& bad) {
     const float E = QK_KAL_E, q = QK_KAL_Q;
     f2 f[5];
     float a[5];
@@ -422,12 +428,13 @@ __device__ __forceinline__ void update_eq(Kal& k, const f2 (&x)[5], f2 e) {
     float xs[5], ys[5];
 #pragma unroll
     for (int j = 0; j < 5; j++) xs[j] = a[j] + ht;
-    if (__builtin_expect(qk_rcp_in_range(xs[0], xs[4]), 1)) {
-#pragma unroll
-        for (int j = 0; j < 5; j++) ys[j] = qk_rcp_fast(xs[j]);
-    } else {
+    if (EXACT) {
 #pragma unroll
         for (int j = 0; j < 5; j++) ys[j] = qk_div_ieee(xs[j]);
+    } else {
+        bad |= !qk_rcp_in_range(xs[0], xs[4]);
+#pragma unroll
+        for (int j = 0; j < 5; j++) ys[j] = qk_rcp_fast(xs[j]);
     }
     float y = ys[0];                                      // 6.19
     k.d[0] = k.d[0] * ((hq * (E + ht)) * y);              // 6.20 (both halves)
@@ -505,12 +512,9 @@ __device__ __forceinline__ void get_job(const float4* in, DataJob& j) {
 // per step: 2x the traffic in profiles/calib.)
 __device__ __forceinline__ float4 ldw(const float4* p) { return *p; }
 
-// One frame of the back wave: lane = channel.  Window slots 1..163 hold
-// dec[mi .. mi+162]; read two slots (16 B) every two steps.
-__device__ __forceinline__ void back_frame(const RxArgs& a, int ch, bool live, int n, int mi,
-                                           int rt, const float2* win, int* rt_next) {
-    const float4* wp = reinterpret_cast<const float4*>(win);
-    Kal k;                                         // kalman_reset, src/kalman.c:42-55
+// kalman_reset, src/kalman.c:42-55
+__device__ __forceinline__ Kal kal_reset() {
+    Kal k;
 #pragma unroll
     for (int i = 0; i < 5; i++) {
         k.eq[i] = k.g[i] = f2{0.0f, 0.0f};
@@ -518,21 +522,30 @@ __device__ __forceinline__ void back_frame(const RxArgs& a, int ch, bool live, i
     }
 #pragma unroll
     for (int i = 0; i < 10; i++) k.u[i] = f2{0.0f, 0.0f};
-    f2 x[5];
-    {
-        const float4 w0 = ldw(wp + 0), w1 = ldw(wp + 1), w2 = ldw(wp + 2);
-        x[0] = f2{w0.z, w0.w};
-        x[1] = f2{w1.x, w1.y};
-        x[2] = f2{w1.z, w1.w};
-        x[3] = f2{w2.x, w2.y};
-        x[4] = f2{w2.z, w2.w};
-    }
-    // equalize(): 128 x train_eq (src/qpsk.c:111-123, src/equalizer.c:45-58)
-    const f2* wp2 = reinterpret_cast<const f2*>(win);
+    return k;
+}
+
+// window slots 1..5 = dec[mi .. mi+4]
+__device__ __forceinline__ void load_x0(const float4* wp, f2 (&x)[5]) {
+    const float4 w0 = ldw(wp + 0), w1 = ldw(wp + 1), w2 = ldw(wp + 2);
+    x[0] = f2{w0.z, w0.w};
+    x[1] = f2{w1.x, w1.y};
+    x[2] = f2{w1.z, w1.w};
+    x[3] = f2{w2.x, w2.y};
+    x[4] = f2{w2.z, w2.w};
+}
+
+constexpr int kForceExact = 64;   // roles bit: take the exact-division path (tests)
+
+#ifndef QPSK_TRAIN_UNROLL
+#define QPSK_TRAIN_UNROLL 4   // steps per loop iteration (register reuse; A/B knob)
+#endif
+
+// 128 x train_eq (src/equalizer.c:45-58) from the window; returns matches
+template <bool EXACT>
+__device__ __forceinline__ int train(Kal& k, f2 (&x)[5], const f2* wp2, bool& bad) {
     int matches = 0;
-    // two steps per iteration: the allocator then alternates the registers of
-    // the loop-carried state instead of copying it back every step
-#pragma unroll 2
+#pragma unroll QPSK_TRAIN_UNROLL
     for (int i = 0; i < QK_NPRE; i++) {
         const f2 nx = wp2[i + 6];                  // slot i+6 (next step)
         const unsigned long long m = i < 64 ? kPreLo : kPreHi;
@@ -541,11 +554,31 @@ __device__ __forceinline__ void back_frame(const RxArgs& a, int ch, bool live, i
 #pragma unroll
         for (int t = 0; t < 5; t++) v = v + cmul(x[t], k.eq[t]);
         const float er = ref - v.x;                // conjf(ref - val) = (ref - vr, vi)
-        update_eq(k, x, f2{er, v.y});
+        update_eq<EXACT>(k, x, f2{er, v.y}, bad);
         if (er * ref > 0.0f) matches++;
 #pragma unroll
         for (int t = 0; t < 4; t++) x[t] = x[t + 1];
         x[4] = nx;
+    }
+    return matches;
+}
+
+// One frame of the back wave: lane = channel.  Window slots 1..163 hold
+// dec[mi .. mi+162]; read two slots (16 B) every two steps.
+__device__ __forceinline__ void back_frame(const RxArgs& a, int ch, bool live, int n, int mi,
+                                           int rt, const float2* win, int* rt_next) {
+    const float4* wp = reinterpret_cast<const float4*>(win);
+    Kal k = kal_reset();
+    f2 x[5];
+    load_x0(wp, x);
+    // equalize(): 128 x train_eq (src/qpsk.c:111-123, src/equalizer.c:45-58)
+    const f2* wp2 = reinterpret_cast<const f2*>(win);
+    bool bad = (a.roles & kForceExact) != 0;
+    int matches = train<false>(k, x, wp2, bad);
+    if (__builtin_expect(__ballot(bad) != 0ull, 0)) {   // recompute the frame exactly
+        k = kal_reset();
+        load_x0(wp, x);
+        matches = train<true>(k, x, wp2, bad);
     }
     const bool valid = live && matches > QK_MATCH_MIN;   // src/qpsk.c:196
     const size_t cf = (size_t)ch * a.F + n;
@@ -583,6 +616,31 @@ __device__ __forceinline__ void back_frame(const RxArgs& a, int ch, bool live, i
     }
 }
 
+// 31 x data_eq + qpsk_demod (src/equalizer.c:64-90, src/qpsk.c:268-271) from
+// the job's window samples xs; returns the raw dibits (bit 2s = Q, 2s+1 = I).
+// Decisions collect in a register; the caller stores the 62 bytes after the
+// loop, so no wait on a store sits inside it.
+template <bool EXACT>
+__device__ __forceinline__ unsigned long long data_steps(Kal& k, f2 (&x)[5], const f2* xs,
+                                                         float2* so, bool& bad) {
+    unsigned long long dib = 0;
+    for (int s = 0; s < QK_NDSYM; s++) {
+        const f2 nx = xs[min(s + 5, 34)];
+        f2 sy = {0.0f, 0.0f};
+#pragma unroll
+        for (int t = 0; t < 5; t++) sy = sy + cmulc(x[t], k.eq[t]);
+        const int dI = sy.x < 0.0f, dQ = sy.y < 0.0f;
+        const f2 cst = {dI ? -1.0f : 1.0f, dQ ? -1.0f : 1.0f};
+        update_eq<EXACT>(k, x, (cst - sy) * 0.1f, bad);
+        dib |= (unsigned long long)(dQ | (dI << 1)) << (2 * s);
+        if (so) so[s] = make_float2(sy.x, sy.y);
+#pragma unroll
+        for (int t = 0; t < 4; t++) x[t] = x[t + 1];
+        x[4] = nx;
+    }
+    return dib;
+}
+
 // ---------------------------------------------------------------- data kernel
 // The 31 data symbols of every valid frame (src/qpsk.c:204-215: data_eq
 // src/equalizer.c:64-90, qpsk_demod src/qpsk.c:268-271, scramble
@@ -593,7 +651,8 @@ __device__ __forceinline__ void back_frame(const RxArgs& a, int ch, bool live, i
 // on it.
 __global__ void __launch_bounds__(256) rx_data_kernel(const float4* jobs, unsigned* njobs,
                                                       const unsigned long long* ks_tab,
-                                                      uint8_t* bits, float2* soft, int parity) {
+                                                      uint8_t* bits, float2* soft, int parity,
+                                                      int force_exact) {
     const unsigned n = njobs[parity];
     const unsigned stride = gridDim.x * blockDim.x;
     for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
@@ -606,23 +665,13 @@ __global__ void __launch_bounds__(256) rx_data_kernel(const float4* jobs, unsign
         for (int t = 0; t < 5; t++) x[t] = xs[t];
         const unsigned long long ks = ks_tab[j.ks];
         float2* so = soft ? soft + j.cf * QK_NDSYM : nullptr;
-        Kal& k = j.k;
-        // decisions collect in a register; the 62 bytes are stored after the
-        // loop, so no wait on a store ever sits inside it
-        unsigned long long dib = 0;
-        for (int s = 0; s < QK_NDSYM; s++) {
-            const f2 nx = xs[min(s + 5, 34)];
-            f2 sy = {0.0f, 0.0f};
+        bool bad = force_exact != 0;
+        unsigned long long dib = data_steps<false>(j.k, x, xs, so, bad);
+        if (__builtin_expect(bad, 0)) {   // recompute the job with IEEE division
+            get_job(jp, j);
 #pragma unroll
-            for (int t = 0; t < 5; t++) sy = sy + cmulc(x[t], k.eq[t]);
-            const int dI = sy.x < 0.0f, dQ = sy.y < 0.0f;
-            const f2 cst = {dI ? -1.0f : 1.0f, dQ ? -1.0f : 1.0f};
-            update_eq(k, x, (cst - sy) * 0.1f);
-            dib |= (unsigned long long)(dQ | (dI << 1)) << (2 * s);   // bit 2s = Q, 2s+1 = I
-            if (so) so[s] = make_float2(sy.x, sy.y);
-#pragma unroll
-            for (int t = 0; t < 4; t++) x[t] = x[t + 1];
-            x[4] = nx;
+            for (int t = 0; t < 5; t++) x[t] = xs[t];
+            dib = data_steps<true>(j.k, x, xs, so, bad);
         }
         dib ^= ks;   // descramble (src/scramble.c:57-84): keystream bits 62g .. 62g+61
         uint16_t* bo = reinterpret_cast<uint16_t*>(bits + j.cf * QK_NBITS);
@@ -923,6 +972,7 @@ extern "C" qpsk_ctx* qpsk_rx_create(int device, int nch, int* err) {
         const int v = !strcmp(pr, "front") ? 1 : !strcmp(pr, "back") ? 2 : 0;
         c->roles = (c->roles & 3) | (v << 4);
     }
+    if (getenv("QPSK_FORCE_EXACT")) c->roles |= kForceExact;   // tests: exact-division path
     if (const char* sh = getenv("QPSK_SHAPE"))
         c->shape_groups = !strcmp(sh, "1x8") ? 1 : !strcmp(sh, "2x4") ? 2 : !strcmp(sh, "4x2") ? 4 : 0;
     int r = herr(hipSetDevice(device));
@@ -1019,7 +1069,8 @@ extern "C" int qpsk_rx_batch_device(qpsk_ctx* c, const int16_t* d_in, int F, uin
     HCHECK(hipGetLastError());
     if (slot >= 0) HCHECK(hipEventRecord(c->ev[slot][1], s));
     hipLaunchKernelGGL(rx_data_kernel, dim3(kDataBlocks), dim3(kDataThreads), 0, s, c->d_jobs,
-                       c->d_njobs, c->d_ks, d_bits, reinterpret_cast<float2*>(d_soft), parity);
+                       c->d_njobs, c->d_ks, d_bits, reinterpret_cast<float2*>(d_soft), parity,
+                       c->roles & kForceExact);
     HCHECK(hipGetLastError());
     if (slot >= 0) HCHECK(hipEventRecord(c->ev[slot][2], s));
     c->frames += (uint64_t)F;

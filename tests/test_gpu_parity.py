@@ -220,3 +220,13 @@ def test_every_workgroup_shape(shape, monkeypatch):
     monkeypatch.setenv("QPSK_SHAPE", shape)
     x = oracle.synth(61, 300, 12, 5.0)
     _vs_oracle(x)
+
+
+def test_exact_division_fallback(monkeypatch):
+    """The Kalman step's fast reciprocal has an exact-division fallback that
+    recomputes a whole frame (rx_kernel) or job (rx_data_kernel) when an
+    operand leaves the fast path's range; QPSK_FORCE_EXACT takes it for every
+    frame, and the outputs must not change."""
+    monkeypatch.setenv("QPSK_FORCE_EXACT", "1")
+    x = oracle.synth(63, 200, 10, 4.0)
+    _vs_oracle(x)
