@@ -8,7 +8,7 @@ TAG=${1:-run}; shift || true
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-B="bench.py --steps 5 --warmup 2 --cpu-channels 0 --verify 0 $*"
+B="bench.py --steps 5 --warmup 2 --cpu-channels 0 --cpu-all-channels 0 --stream-chunks 0 --verify 0 $*"
 run() { # name, rocprof args...
   local name=$1; shift
   timeout -k 10 300 rocprofv3 "$@" --output-format csv -d $OUT/$name -o $name -- python3 $B \

@@ -1,10 +1,15 @@
 """Summarise a profiles/profile.sh run: per-kernel average duration and
-per-dispatch PMC averages for rx_step_kernel, HBM traffic per launch with the
-gfx950 FETCH_SIZE correction (MI355X_MICROARCH.md 'HBM': FETCH_SIZE counts
-half the bytes of wide coalesced reads -> x2), writes profiles/<tag>_summary.md
-and profiles/pmc_traffic.json.
+per-dispatch PMC averages for rx_kernel / rx_data_kernel, HBM traffic per
+launch with the gfx950 FETCH_SIZE correction (MI355X_MICROARCH.md 'HBM':
+FETCH_SIZE counts half the bytes of wide coalesced reads -> x2), writes
+profiles/<tag>_summary.md and profiles/pmc_traffic.json.
 
-    python profiles/summarize.py gpurun_out/prof_v1 TAG CHANNELS FRAMES [KERNEL]
+    python profiles/summarize.py gpurun_out/prof_v1 TAG CHANNELS FRAMES [SKIP [COUNT]]
+
+Only the bench's timed launches are summarised: per kernel, the launches
+SKIP .. SKIP+COUNT-1 in dispatch order (default 2 and 5 = bench.py's
+--warmup 2 --steps 5 as profile.sh runs it).  Later launches of the same
+kernels (other batch sizes) and the cold warmup launches are excluded.
 """
 import csv
 import glob
@@ -15,8 +20,9 @@ import sys
 from collections import defaultdict
 
 d, tag, nch, nfr = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4])
-K = sys.argv[5] if len(sys.argv) > 5 else "rx_kernel"
-KD = "rx_data_kernel"
+SKIP = int(sys.argv[5]) if len(sys.argv) > 5 else 2
+COUNT = int(sys.argv[6]) if len(sys.argv) > 6 else 5
+K, KD = "rx_kernel", "rx_data_kernel"
 
 
 def rows(pattern):
@@ -26,47 +32,54 @@ def rows(pattern):
     return out
 
 
-def stats(name):
-    r = rows(f"{name}/**/*kernel_stats.csv")
-    return {short(x["Name"]): (int(x["Calls"]), float(x["AverageNs"])) for x in r}
-
-
 def short(name):
-    m = re.search(r"(\w+)\(", name.replace("(anonymous namespace)", "anon"))
+    name = re.sub(r"<[^<>]*>", "", name.replace("(anonymous namespace)", "anon"))   # template args
+    m = re.search(r"(\w+)\(", name)
     return m.group(1) if m else name
 
 
-def counters(name, kern=None):
-    kern = kern or K
-    acc = defaultdict(list)
-    for x in rows(f"{name}/**/*counter_collection.csv"):
-        if short(x["Kernel_Name"]) == kern:
-            acc[x["Counter_Name"]].append(float(x["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in acc.items()}
+def launches(run):
+    """{kernel: [(dispatch_id, duration ns)]} of the selected launches"""
+    per = defaultdict(list)
+    for x in rows(f"{run}/**/*kernel_trace.csv"):
+        per[short(x["Kernel_Name"])].append(
+            (int(x["Dispatch_Id"]), int(x["End_Timestamp"]) - int(x["Start_Timestamp"])))
+    return {k: sorted(v)[SKIP:SKIP + COUNT] for k, v in per.items()}
 
 
-lines = [f"# rocprofv3 summary: {tag} ({nch} channels x {nfr} frames per launch)", ""]
-st = stats("stats")
-lines += ["## Kernel durations (kernel-trace --stats)", "",
-          "| kernel | calls | avg us |", "|---|---|---|"]
-for k, (c, a) in sorted(st.items(), key=lambda t: -t[1][0] * t[1][1]):
-    lines.append(f"| {k} | {c} | {a / 1e3:.1f} |")
+def avg_ns(run, kern):
+    sel = launches(run).get(kern, [])
+    return sum(t for _, t in sel) / len(sel) if sel else 0.0
+
+
+def counters(run, kern):
+    ids = {i for i, _ in launches(run).get(kern, [])}
+    acc = defaultdict(lambda: defaultdict(float))   # counter -> dispatch -> sum over agents/dims
+    for x in rows(f"{run}/**/*counter_collection.csv"):
+        if short(x["Kernel_Name"]) == kern and int(x["Dispatch_Id"]) in ids:
+            acc[x["Counter_Name"]][int(x["Dispatch_Id"])] += float(x["Counter_Value"])
+    return {k: sum(v.values()) / len(v) for k, v in acc.items()}
+
+
+lines = [f"# rocprofv3 summary: {tag} ({nch} channels x {nfr} frames per launch)", "",
+         f"Launches {SKIP}..{SKIP + COUNT - 1} of each kernel (the bench's timed steps; "
+         f"the first {SKIP} are its untimed warmup).", ""]
+t_ns, t_dns = avg_ns("stats", K), avg_ns("stats", KD)
+lines += ["## Kernel durations (kernel-trace)", "", "| kernel | launches | avg us |", "|---|---|---|",
+          f"| {K} | {COUNT} | {t_ns / 1e3:.1f} |", f"| {KD} | {COUNT} | {t_dns / 1e3:.1f} |"]
 for ab in ("abl_back", "abl_front"):
-    s = stats(ab)
-    if K in s:
-        lines.append(f"| {K} [{ab}: only the {ab[4:]} role runs] | {s[K][0]} | {s[K][1] / 1e3:.1f} |")
+    if glob.glob(os.path.join(d, ab)):
+        lines.append(f"| {K} [{ab}: only the {ab[4:]} role runs] | {COUNT} | {avg_ns(ab, K) / 1e3:.1f} |")
 c, cd = {}, {}
 for p in ("fetch", "write", "sq", "lds"):
-    c.update(counters(p))
+    c.update(counters(p, K))
     cd.update(counters(p, KD))
-t_ns = st[K][1]
-t_dns = st[KD][1] if KD in st else 0.0
 # per step: rx_kernel + rx_data_kernel (the data symbols of the valid frames)
 fetch_b = (c.get("FETCH_SIZE", 0) + cd.get("FETCH_SIZE", 0)) * 1024 * 2   # KB, x2 gfx950 correction
 write_b = (c.get("WRITE_SIZE", 0) + cd.get("WRITE_SIZE", 0)) * 1024
 alg = nch * nfr * 3823
 t_step = t_ns + t_dns
-lines += ["", f"## Counters per dispatch (averages)", "", f"| counter | {K} | {KD} |", "|---|---|---|"]
+lines += ["", "## Counters per dispatch (averages)", "", f"| counter | {K} | {KD} |", "|---|---|---|"]
 for k in sorted(c):
     lines.append(f"| {k} | {c[k]:.4g} | {cd.get(k, float('nan')):.4g} |")
 lines += ["", "## Derived (per step = one rx_kernel + one rx_data_kernel launch)", "",
