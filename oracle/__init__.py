@@ -57,6 +57,9 @@ def cpu_lib():
         lib.qc_rx_batch.restype = C.c_long
         lib.qc_rx_batch.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
                                     C.c_void_p, C.c_int]
+        lib.qc_rx_batch_mode.restype = C.c_long
+        lib.qc_rx_batch_mode.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
+                                         C.c_void_p, C.c_int, C.c_int]
         lib.qc_synth_batch.restype = None
         lib.qc_synth_batch.argtypes = [C.c_uint64, C.c_uint32, C.c_int, C.c_double,
                                        C.c_void_p, C.c_long, C.c_int]
@@ -66,22 +69,33 @@ def cpu_lib():
     return _cpu
 
 
-def ref_available() -> bool:
-    return os.path.exists(os.path.join(HERE, "_ref", "libqpsk_ref.so"))
+# receiver semantics (cpu_ref.h QC_MODE_*; singlecarrier_amd.MODE_*)
+MODE_REF = 0      # the reference as built (gcc -O2, "model A" overflow)
+MODE_DEC752 = 1   # decimated_frame[752] ("intended semantics", NOT reference parity)
+_REF_LIBS = {MODE_REF: "libqpsk_ref.so", MODE_DEC752: "libqpsk_ref752.so"}
 
 
-def ref_lib():
+def ref_available(mode: int = MODE_REF) -> bool:
+    return os.path.exists(os.path.join(HERE, "_ref", _REF_LIBS[mode]))
+
+
+def ref_lib(mode: int = MODE_REF):
+    """The reference build for `mode`: libqpsk_ref.so, or libqpsk_ref752.so (the
+    same unmodified sources with decimated_frame followed by owned padding,
+    oracle/ref/dec752.ld)."""
     global _ref
     if _ref is None:
-        lib = C.CDLL(os.path.join(HERE, "_ref", "libqpsk_ref.so"))
+        _ref = {}
+    if mode not in _ref:
+        lib = C.CDLL(os.path.join(HERE, "_ref", _REF_LIBS[mode]))
         lib.ref_rx_stream.restype = C.c_int
         lib.ref_rx_stream.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
         lib.ref_rx_batch.restype = C.c_int
         lib.ref_rx_batch.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
         lib.ref_layout_gap.restype = C.c_long
         lib.ref_log_set.argtypes = [C.c_void_p, C.c_size_t]
-        _ref = lib
-    return _ref
+        _ref[mode] = lib
+    return _ref[mode]
 
 
 def _frames(x):
@@ -92,7 +106,7 @@ def _frames(x):
     return x
 
 
-def cpu_rx(x, threads: int = 0, trace: bool = False):
+def cpu_rx(x, threads: int = 0, trace: bool = False, mode: int = MODE_REF):
     """Restatement over x [nch][nframes][1880] (or [nframes][1880]).
     Returns bits [nch][nframes][62] u8, valid [nch][nframes] u8, trace|None."""
     x = _frames(x)
@@ -101,15 +115,15 @@ def cpu_rx(x, threads: int = 0, trace: bool = False):
     valid = np.zeros((nch, nf), np.uint8)
     tr = np.zeros((nch, nf), TRACE_DTYPE) if trace else None
     threads = threads or min(16, os.cpu_count() or 1)
-    cpu_lib().qc_rx_batch(_p(x), nch, nf, _p(bits), _p(valid), _p(tr), threads)
+    cpu_lib().qc_rx_batch_mode(_p(x), nch, nf, _p(bits), _p(valid), _p(tr), threads, mode)
     return bits, valid, tr
 
 
-def ref_rx(x, trace: bool = False, log: bool = False):
+def ref_rx(x, trace: bool = False, log: bool = False, mode: int = MODE_REF):
     """The unmodified reference, one channel at a time (single thread)."""
     x = _frames(x)
     nch, nf, _ = x.shape
-    lib = ref_lib()
+    lib = ref_lib(mode)
     bits = np.zeros((nch, nf, NBITS), np.uint8)
     valid = np.zeros((nch, nf), np.uint8)
     tr = np.zeros((nch, nf), REF_TRACE_DTYPE) if trace else None
@@ -120,26 +134,26 @@ def ref_rx(x, trace: bool = False, log: bool = False):
         r = lib.ref_rx_stream(_p(x[c]), nf, _p(bits[c]), _p(valid[c]),
                               _p(tr[c]) if trace else None)
         if r < 0:
-            raise RuntimeError("reference static layout is not model A")
+            raise RuntimeError("reference static layout is not the expected one")
     if log:
         lib.ref_log_set(None, 0)
     return (bits, valid, tr, buf.value.decode()) if log else (bits, valid, tr)
 
 
-def ref_stages(x):
+def ref_stages(x, mode: int = MODE_REF):
     """One channel through the reference, frame by frame, returning the
     reference's own buffers after each call: dec [nf][290][2] (decimated_frame
     [0..289]) and mixed [nf][1880][2] (input_frame[1880..3759])."""
     x = _frames(x)[0]
     nf = x.shape[0]
-    lib = ref_lib()
+    lib = ref_lib(mode)
     lib.ref_rx_reset.restype = C.c_int
     lib.ref_rx_frame.restype = C.c_int
     lib.ref_rx_frame.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
     lib.ref_peek_dec.argtypes = [C.c_void_p]
     lib.ref_peek_mixed.argtypes = [C.c_void_p]
     if lib.ref_rx_reset() != 0:
-        raise RuntimeError("reference static layout is not model A")
+        raise RuntimeError("reference static layout is not the expected one")
     dec = np.zeros((nf, 290, 2), np.float32)
     mixed = np.zeros((nf, FRAME, 2), np.float32)
     bits = np.zeros((nf, NBITS), np.uint8)

@@ -16,6 +16,11 @@
  *    [0..101] and {5i+rt} are observable (A.6) and only those are computed.
  *  - decimation with the gcc -O2 overflow semantics ("model A", A.4):
  *    dec[0..187] = D_{n-1}, dec[188..] = fir_out_n[0..], D_n[i] = fir_out_n[5i+rt].
+ *    QC_MODE_DEC752 instead gives decimated_frame the 752 entries the loop at
+ *    src/qpsk.c:157-162 writes: dec[0..375] = D_{n-1}[0..375] and nothing of
+ *    frame n's own decimation is read before frame n+1, so the observable
+ *    dec[0..289] = D_{n-1}[0..289], D_n[i] = fir_out_n[5i+rt] (5i+rt <= 1700 <
+ *    1880: always a filtered sample).
  *  - correlator (src/qpsk.c:88-96): preamble symbols are p+pj with p = +-1, so
  *    each product is p*(dr-di, di+dr) exactly (A.3).
  *  - invalid frames skip data_eq (unobservable, A.6) but advance the keystream
@@ -109,11 +114,14 @@ static void init_tables(void) {
 
 /* ------------------------------------------------------------------ RX */
 
-void qc_chan_init(qc_chan_t *ch) {
+void qc_chan_init_mode(qc_chan_t *ch, int mode) {
     pthread_once(&g_once, init_tables);
     memset(ch, 0, sizeof(*ch));
     ch->rx_timing = 3;  /* FINE_TIMING_OFFSET, headers/qpsk_internal.h:23 */
+    ch->mode = mode;
 }
+
+void qc_chan_init(qc_chan_t *ch) { qc_chan_init_mode(ch, QC_MODE_REF); }
 
 /* mixed sample m_k[t] (src/qpsk.c:139-144) of frame k with parity sign */
 static inline void mix(const int16_t *x, uint32_t k, int t, float out[2]) {
@@ -260,9 +268,12 @@ int qc_rx_frame(qc_chan_t *ch, const int16_t in[QC_FRAME], uint8_t bits[QC_BITS]
                 qc_trace_t *tr) {
     const uint32_t n = ch->frame;
     const int rt = ch->rx_timing;
-    /* M[-48..1190]: m_{n-2}[1832..1879] ++ m_{n-1}[0..1190] (zero before frame 0) */
-    enum { LO = QC_NTAPS - 1, HI = 5 * (QC_DEC - 1) + 255 };
-    float Mbuf[LO + HI + 1][2];
+    const int d752 = ch->mode == QC_MODE_DEC752;
+    /* M[-48..hi]: m_{n-2}[1832..1879] ++ m_{n-1}[0..hi] (zero before frame 0);
+     * hi = 1190 (model A, D_n[0..187]) or 1700 (dec752, D_n[0..289]) */
+    enum { LO = QC_NTAPS - 1, HIMAX = 5 * (QC_DEC752 - 1) + 255 };
+    const int HI = d752 ? HIMAX : 5 * (QC_DEC - 1) + 255;
+    float Mbuf[LO + HIMAX + 1][2];
     float (*M)[2] = Mbuf + LO;
     for (int t = -LO; t <= HI; t++) {
         if (t < 0) {
@@ -273,11 +284,16 @@ int qc_rx_frame(qc_chan_t *ch, const int16_t in[QC_FRAME], uint8_t bits[QC_BITS]
             else M[t][0] = M[t][1] = 0.0f;
         }
     }
-    /* dec[0..289] (model A) */
-    float dec[QC_DEC + 102][2];
-    memcpy(dec, ch->dprev, sizeof ch->dprev);
-    for (int j = 0; j < 102; j++) fir_at(M + j - LO, dec[QC_DEC + j]);
-    for (int i = 0; i < QC_DEC; i++) fir_at(M + 5 * i + rt - LO, ch->dprev[i]);
+    /* dec[0..289] */
+    float dec[QC_DEC752][2];
+    if (d752) {   /* dec = D_{n-1}[0..289] */
+        memcpy(dec, ch->dprev, sizeof ch->dprev);
+        for (int i = 0; i < QC_DEC752; i++) fir_at(M + 5 * i + rt - LO, ch->dprev[i]);
+    } else {      /* model A: dec = D_{n-1}[0..187] ++ fir_out_n[0..101] */
+        memcpy(dec, ch->dprev, sizeof(float[QC_DEC][2]));
+        for (int j = 0; j < 102; j++) fir_at(M + j - LO, dec[QC_DEC + j]);
+        for (int i = 0; i < QC_DEC; i++) fir_at(M + 5 * i + rt - LO, ch->dprev[i]);
+    }
 
     /* preamble hunt, src/qpsk.c:172-183 */
     float T[255], U[255];
@@ -344,7 +360,7 @@ int qc_rx_frame(qc_chan_t *ch, const int16_t in[QC_FRAME], uint8_t bits[QC_BITS]
 
 typedef struct {
     const int16_t *in;
-    int nch, nframes, c0, c1;
+    int nch, nframes, c0, c1, mode;
     uint8_t *bits, *valid;
     qc_trace_t *tr;
     long nvalid;
@@ -355,7 +371,7 @@ static void *batch_worker(void *arg) {
     qc_chan_t *ch = (qc_chan_t *)malloc(sizeof(qc_chan_t));
     j->nvalid = 0;
     for (int c = j->c0; c < j->c1; c++) {
-        qc_chan_init(ch);
+        qc_chan_init_mode(ch, j->mode);
         for (int n = 0; n < j->nframes; n++) {
             size_t cf = (size_t)c * j->nframes + n;
             int v = qc_rx_frame(ch, j->in + cf * QC_FRAME, j->bits + cf * QC_BITS,
@@ -370,6 +386,11 @@ static void *batch_worker(void *arg) {
 
 long qc_rx_batch(const int16_t *in, int nch, int nframes, uint8_t *bits,
                  uint8_t *valid, qc_trace_t *tr, int nthreads) {
+    return qc_rx_batch_mode(in, nch, nframes, bits, valid, tr, nthreads, QC_MODE_REF);
+}
+
+long qc_rx_batch_mode(const int16_t *in, int nch, int nframes, uint8_t *bits,
+                      uint8_t *valid, qc_trace_t *tr, int nthreads, int mode) {
     pthread_once(&g_once, init_tables);
     if (nthreads < 1) nthreads = 1;
     if (nthreads > nch) nthreads = nch > 0 ? nch : 1;
@@ -377,7 +398,7 @@ long qc_rx_batch(const int16_t *in, int nch, int nframes, uint8_t *bits,
     pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
     for (int t = 0; t < nthreads; t++) {
         jobs[t] = (batch_job_t){in, nch, nframes, (int)((long)nch * t / nthreads),
-                                (int)((long)nch * (t + 1) / nthreads), bits, valid, tr, 0};
+                                (int)((long)nch * (t + 1) / nthreads), mode, bits, valid, tr, 0};
         if (nthreads > 1) pthread_create(&th[t], NULL, batch_worker, &jobs[t]);
         else batch_worker(&jobs[t]);
     }

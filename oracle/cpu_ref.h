@@ -29,12 +29,23 @@ extern "C" {
 #define QC_NTAPS      49     /* NTAPS               headers/fir.h:16           */
 #define QC_PACKET     2783   /* one TX packet: 640 + 8*155 + 903 samples       */
 
+#define QC_DEC752     290    /* observable carried symbols, dec752 mode        */
+
+/* Receiver semantics. */
+#define QC_MODE_REF     0    /* the reference as built: gcc -O2 "model A" overflow */
+#define QC_MODE_DEC752  1    /* decimated_frame with the 752 entries its loop
+                                assumes (src/qpsk.c:157-162): NOT reference
+                                parity; pinned by the layout-padded reference
+                                build oracle/_ref/libqpsk_ref752.so           */
+
 /* Explicit per-channel receiver state (the reference keeps it in statics,
  * src/qpsk.c:37-53, src/scramble.c:41-42). */
 typedef struct {
     int32_t rx_timing;          /* src/qpsk.c:53, starts at 3               */
     uint32_t frame;             /* frames received so far                   */
-    float dprev[QC_DEC][2];     /* D_{n-1}: decimated symbols carried over  */
+    int32_t mode;               /* QC_MODE_*                                */
+    float dprev[QC_DEC752][2];  /* D_{n-1}: decimated symbols carried over
+                                   (model A uses the first QC_DEC)          */
     int16_t hist[2][QC_FRAME];  /* hist[1] = x_{n-1}, hist[0] = x_{n-2}     */
 } qc_chan_t;
 
@@ -47,6 +58,7 @@ typedef struct {
 } qc_trace_t;
 
 void qc_chan_init(qc_chan_t *ch);
+void qc_chan_init_mode(qc_chan_t *ch, int mode);
 /* One qpsk_rx_frame() call.  bits[62] written (zero when invalid). */
 int qc_rx_frame(qc_chan_t *ch, const int16_t in[QC_FRAME], uint8_t bits[QC_BITS],
                 qc_trace_t *tr);
@@ -55,6 +67,9 @@ int qc_rx_frame(qc_chan_t *ch, const int16_t in[QC_FRAME], uint8_t bits[QC_BITS]
  * tr [nch][nframes] or NULL.  Returns the number of valid frames. */
 long qc_rx_batch(const int16_t *in, int nch, int nframes, uint8_t *bits,
                  uint8_t *valid, qc_trace_t *tr, int nthreads);
+/* Same, with the receiver semantics `mode` (QC_MODE_*). */
+long qc_rx_batch_mode(const int16_t *in, int nch, int nframes, uint8_t *bits,
+                      uint8_t *valid, qc_trace_t *tr, int nthreads, int mode);
 
 /* Mixer table P[t] = R^(t+1) (fp32 recurrence, src/qpsk.c:139), KAT access. */
 void qc_mixer_table(float p[QC_FRAME][2]);

@@ -7,7 +7,13 @@ streams regenerated from a seed by the oracle's TX restatement (the input's
 sha256 is stored so the generator itself is pinned).  Every expected output
 below comes from oracle/_ref/libqpsk_ref.so, i.e. the reference's own code.
 
-    python tests/golden/make_golden.py
+    python tests/golden/make_golden.py            # everything
+    python tests/golden/make_golden.py --dec752   # only the dec752-mode fixtures
+
+The dec752 fixtures ("intended semantics"; NOT reference
+parity) come from oracle/_ref/libqpsk_ref752.so: the same unmodified reference
+sources, linked so that decimated_frame owns the 752 entries its decimation
+loop writes (oracle/ref/dec752.ld).
 """
 import hashlib
 import json
@@ -38,12 +44,59 @@ PREAMBLE = [-1, 1, 1, -1, -1, 1, 1, 1, -1, 1, -1, -1, 1, 1, -1, -1, 1, 1, -1, 1,
             -1, 1, -1, 1, -1, -1, -1, 1]
 
 
+DEC752_CASES = [  # (name, seed, nch, nframes, ebn0_db)
+    ("synth_d752_s1_clean", 11, 48, 16, 1000.0),
+    ("synth_d752_s2_eb4", 12, 48, 16, 4.0),
+]
+
+
 def bitstr(b):
     return "".join(str(int(v)) for v in b)
 
 
+def _synth_golden(name, seed, nch, nfr, eb, mode):
+    xs = oracle.synth(seed, nch, nfr, eb)
+    b, v, t = oracle.ref_rx(xs, trace=True, mode=mode)
+    soft = np.where(v[..., None, None].astype(bool), t["soft"], 0).astype(np.float32)
+    np.savez_compressed(
+        os.path.join(HERE, name + ".npz"), seed=seed, nch=nch, nframes=nfr, ebn0_db=eb,
+        mode=mode, input_sha256=hashlib.sha256(xs.tobytes()).hexdigest(),
+        bits=np.packbits(b, axis=-1), valid=v, max_index=t["max_index"],
+        matches=t["matches"], rx_timing=t["rx_timing"], soft=soft)
+    print(name, "valid frac %.3f" % v.mean())
+
+
+def dec752():
+    """Fixtures of the dec752 mode from the layout-padded reference build."""
+    assert oracle.ref_available(oracle.MODE_DEC752)
+    raw = np.fromfile(os.path.join(HERE, "preamble_qpsk_8k.raw"), np.int16)
+    nf = raw.size // oracle.FRAME
+    x = raw[: nf * oracle.FRAME].reshape(1, nf, oracle.FRAME)
+    bits, valid, tr = oracle.ref_rx(x, trace=True, mode=oracle.MODE_DEC752)
+    recs = b"".join(np.concatenate([bits[0, n], np.zeros(496 - 62, np.uint8)]).tobytes()
+                    for n in range(nf) if valid[0, n])
+    exp = {
+        "mode": "dec752 (decimated_frame[752]; not reference parity)",
+        "input": "preamble_qpsk_8k.raw",
+        "input_md5": hashlib.md5(raw.tobytes()).hexdigest(),
+        "frames": int(nf),
+        "output_bytes": len(recs),
+        "output_md5": hashlib.md5(recs).hexdigest(),
+        "trace": [{k: int(tr[0, n][k]) for k in ("max_index", "matches", "valid", "rx_timing")}
+                  for n in range(nf)],
+        "soft": {str(n): tr[0, n]["soft"].tolist() for n in range(nf) if valid[0, n]},
+    }
+    with open(os.path.join(HERE, "sample_expected_dec752.json"), "w") as f:
+        json.dump(exp, f, indent=1)
+    for name, seed, nch, nfr, eb in DEC752_CASES:
+        _synth_golden(name, seed, nch, nfr, eb, oracle.MODE_DEC752)
+    print("sample (dec752):", exp["output_md5"], exp["output_bytes"], "B")
+
+
 def main():
     oracle.build(ref=True)
+    if "--dec752" in sys.argv[1:]:
+        return dec752()
     assert oracle.ref_available()
     # 1. the reference's sample capture, through the reference driver semantics
     src = "/root/reference/preamble_qpsk_8k.raw"
@@ -83,15 +136,7 @@ def main():
 
     # 3. seeded synthetic channels (noiseless and AWGN)
     for name, seed, nch, nfr, eb in SYNTH_CASES:
-        xs = oracle.synth(seed, nch, nfr, eb)
-        b, v, t = oracle.ref_rx(xs, trace=True)
-        soft = np.where(v[..., None, None].astype(bool), t["soft"], 0).astype(np.float32)
-        np.savez_compressed(
-            os.path.join(HERE, name + ".npz"), seed=seed, nch=nch, nframes=nfr, ebn0_db=eb,
-            input_sha256=hashlib.sha256(xs.tobytes()).hexdigest(),
-            bits=np.packbits(b, axis=-1), valid=v, max_index=t["max_index"],
-            matches=t["matches"], rx_timing=t["rx_timing"], soft=soft)
-        print(name, "valid frac %.3f" % v.mean())
+        _synth_golden(name, seed, nch, nfr, eb, oracle.MODE_REF)
     # 4. reference transmitter (src/qpsk.c:278-342): 3 packets, seeded dibits
     pre = np.array([complex(p, p) for p in PREAMBLE], np.complex64)
     rng = np.random.default_rng(42)
@@ -108,6 +153,7 @@ def main():
                         preamble=np.array([p for _, p in syms]),
                         lengths=np.array([len(s) for s, _ in syms]), samples=np.concatenate(out))
     print("sample:", exp["output_md5"], exp["output_bytes"], "B")
+    dec752()
 
 
 if __name__ == "__main__":
