@@ -66,6 +66,9 @@ def parse():
     ap.add_argument("--ebn0", type=float, default=1000.0, help=">= 100: noiseless")
     ap.add_argument("--seed", type=int, default=3)
     ap.add_argument("--strong", action="store_true", help="split --channels across ranks")
+    ap.add_argument("--mode", choices=("reference", "dec752"), default="reference",
+                    help="receiver semantics: reference parity (default) or dec752 "
+                         "(decimated_frame[752], SURVEY.md 8f rank 3; not reference parity)")
     ap.add_argument("--cpu-channels", type=int, default=4096,
                     help="channels of the bounded CPU-baseline sample (0: skip)")
     ap.add_argument("--verify", type=int, default=256,
@@ -127,15 +130,20 @@ def _pack62(bits):
     return w
 
 
+def _ref_name(mode: int) -> str:
+    return ("unmodified reference (oracle/_ref, gcc -O2)" if mode == 0 else
+            "unmodified reference sources, dec752 layout (oracle/_ref/libqpsk_ref752.so)")
+
+
 def _ref_timed(args):
     """One host process of the all-cores baseline: regenerate its channels of
     the benchmark workload (oracle.synth == the bench generator) and time the
     unmodified reference over them, one channel after another."""
     import oracle
-    seed, c0, n, nf, ebn0 = args
+    seed, c0, n, nf, ebn0, mode = args
     x = oracle.synth(seed, n, nf, ebn0, c0=c0, threads=1)
     t = time.perf_counter()
-    oracle.ref_rx(x)
+    oracle.ref_rx(x, mode=mode)
     return n * nf * FRAME, time.perf_counter() - t
 
 
@@ -221,7 +229,7 @@ def main():
     if rank0 and world == 1 and args.cpu_all_channels > 0 and args.cpu_procs > 1:
         import multiprocessing as mp
         import oracle
-        if oracle.ref_available():
+        if oracle.ref_available(1 if args.mode == "dec752" else 0):
             pool = mp.get_context("spawn").Pool(args.cpu_procs)   # before any GPU use
 
     import torch
@@ -256,7 +264,8 @@ def main():
         del x2
     bits = torch.empty((nch, nf, 62), dtype=torch.uint8, device=x.device)
     valid = torch.empty((nch, nf), dtype=torch.uint8, device=x.device)
-    rx = sc.Receiver(nch, device=local)
+    mode = sc.MODE_DEC752 if args.mode == "dec752" else sc.MODE_REFERENCE
+    rx = sc.Receiver(nch, device=local, mode=mode)
 
     for _ in range(args.warmup):
         rx.demod_device(x, bits, valid)
@@ -318,7 +327,8 @@ def main():
         # the timed context advanced (warmup + steps) batches of the same
         # input: the oracle replays that whole stream for the first k channels
         reps = args.warmup + args.steps
-        exp_bits, exp_valid, _ = oracle.cpu_rx(np.concatenate([x_host[:k]] * reps, axis=1))
+        exp_bits, exp_valid, _ = oracle.cpu_rx(np.concatenate([x_host[:k]] * reps, axis=1),
+                                               mode=mode)
         same_input = bool((oracle.synth(args.seed, k, nf, args.ebn0, c0=c0) == x_host[:k]).all())
         verified = bool(same_input and (bits[:k].cpu().numpy() == exp_bits[:, -nf:]).all()
                         and (valid[:k].cpu().numpy() == exp_valid[:, -nf:]).all())
@@ -326,7 +336,7 @@ def main():
     # streaming ingest (include/qpsk_stream.h): host chunks through pinned slots,
     # H2D / receive / D2H overlapped.  PCIe-inclusive; reported, never `value`.
     stream = None
-    if args.stream_chunks > 0 and rank == 0:
+    if args.stream_chunks > 0 and rank == 0 and mode == sc.MODE_REFERENCE:
         fpc = min(args.stream_frames, nf)
         st = sc.Stream(nch, fpc, nslot=3, device=local)
         for _ in range(3):   # untimed: fill every slot's pinned buffer once
@@ -354,17 +364,17 @@ def main():
         import oracle
         k = min(args.cpu_channels, nch)
         sample = x_host[:k]
-        if oracle.ref_available():
+        if oracle.ref_available(mode):
             t = time.perf_counter()
-            oracle.ref_rx(sample)
+            oracle.ref_rx(sample, mode=mode)
             dt = time.perf_counter() - t
             cpu = {"value": round(k * nf * FRAME / dt / 1e6, 3), "unit": "Msamples/s",
                    "cores": 1, "kind": "reference",
-                   "sample": f"{k} of the {nch} channels x {nf} frames, unmodified reference "
-                             f"(oracle/_ref, gcc -O2), one channel after another, {dt:.1f} s"}
+                   "sample": f"{k} of the {nch} channels x {nf} frames, {_ref_name(mode)}, one channel "
+                             f"after another, {dt:.1f} s"}
         else:
             t = time.perf_counter()
-            oracle.cpu_rx(sample, threads=1)
+            oracle.cpu_rx(sample, threads=1, mode=mode)
             dt = time.perf_counter() - t
             cpu = {"value": round(k * nf * FRAME / dt / 1e6, 3), "unit": "Msamples/s",
                    "cores": 1, "kind": "port",
@@ -374,7 +384,7 @@ def main():
     if pool is not None:
         k = min(args.cpu_all_channels, nch)
         bounds = np.linspace(0, k, args.cpu_procs + 1).astype(int)
-        jobs = [(args.seed, c0 + int(a), int(b - a), nf, args.ebn0)
+        jobs = [(args.seed, c0 + int(a), int(b - a), nf, args.ebn0, mode)
                 for a, b in zip(bounds[:-1], bounds[1:]) if b > a]
         res = pool.map(_ref_timed, jobs)
         pool.close()
@@ -382,8 +392,8 @@ def main():
         tmx = max(r[1] for r in res)
         cpu_all = {"value": round(tot / tmx / 1e6, 3), "unit": "Msamples/s",
                    "cores": len(jobs), "kind": "reference",
-                   "sample": f"{k} of the {nch} channels x {nf} frames, unmodified reference "
-                             f"(oracle/_ref, gcc -O2), {len(jobs)} host processes, "
+                   "sample": f"{k} of the {nch} channels x {nf} frames, {_ref_name(mode)}, "
+                             f"{len(jobs)} host processes, "
                              f"slowest {tmx:.1f} s"}
 
     if rank == 0:
@@ -400,7 +410,8 @@ def main():
                                    f"(C3{'/C4' if world > 1 else ''})",
                        "channels_per_gpu": nch, "channels_total": total_ch, "frames": nf,
                        "samples_per_step": int(total_ch * nf * FRAME),
-                       "parallelism": f"channel shards x{world}, no collective"},
+                       "parallelism": f"channel shards x{world}, no collective",
+                       "mode": args.mode},
             "roofline": roofline, "valu": valu, "cpu_baseline": cpu,
             "cpu_baseline_all_cores": cpu_all,
             "region_ms_per_step": round(region_ms / args.steps, 3),

@@ -44,14 +44,30 @@ enum {
     QPSK_EHIP = -1000,    /* QPSK_EHIP - hipError_t */
 };
 
+/* Receiver semantics of a context. */
+enum {
+    QPSK_MODE_REFERENCE = 0,  /* bit-identical to the reference as built (gcc -O2:
+                                 the decimated_frame[562] overflow of
+                                 src/qpsk.c:157-162 aliases input_frame) */
+    QPSK_MODE_DEC752 = 1,     /* "intended semantics": decimated_frame with the
+                                 752 entries its loop writes.  A working receiver
+                                 variant, NOT reference parity; equal to the
+                                 unmodified reference sources linked with that
+                                 array padded (oracle/ref/dec752.ld) */
+};
+
 /* Create a receiver for nch channels on HIP device `device`, in the reference's
  * initial RX state (src/qpsk.c:427-434).  Returns NULL on failure; *err (if
- * non-NULL) receives the error code. */
+ * non-NULL) receives the error code.  qpsk_rx_create() is
+ * qpsk_rx_create_mode(device, nch, QPSK_MODE_REFERENCE, err). */
 qpsk_ctx *qpsk_rx_create(int device, int nch, int *err);
+qpsk_ctx *qpsk_rx_create_mode(int device, int nch, int mode, int *err);
 void qpsk_rx_destroy(qpsk_ctx *ctx);
 /* Back to the initial state (all channels), as after qpsk_rx_create. */
 int qpsk_rx_reset(qpsk_ctx *ctx);
 int qpsk_rx_channels(const qpsk_ctx *ctx);
+/* QPSK_MODE_* of the context. */
+int qpsk_rx_mode(const qpsk_ctx *ctx);
 /* Frames received so far by every channel of the context. */
 uint64_t qpsk_rx_frames(const qpsk_ctx *ctx);
 

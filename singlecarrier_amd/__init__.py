@@ -64,6 +64,9 @@ def lib():
         vp, i32, u64 = C.c_void_p, C.c_int, C.c_uint64
         L.qpsk_rx_create.restype = vp
         L.qpsk_rx_create.argtypes = [i32, i32, C.POINTER(C.c_int)]
+        L.qpsk_rx_create_mode.restype = vp
+        L.qpsk_rx_create_mode.argtypes = [i32, i32, i32, C.POINTER(C.c_int)]
+        L.qpsk_rx_mode.argtypes = [vp]
         L.qpsk_rx_destroy.argtypes = [vp]
         L.qpsk_rx_reset.argtypes = [vp]
         L.qpsk_rx_channels.argtypes = [vp]
@@ -103,7 +106,7 @@ def lib():
     return _lib
 
 
-SYMBOLS = ["qpsk_rx_create", "qpsk_rx_destroy", "qpsk_rx_reset", "qpsk_rx_channels",
+SYMBOLS = ["qpsk_rx_create", "qpsk_rx_create_mode", "qpsk_rx_mode", "qpsk_rx_destroy", "qpsk_rx_reset", "qpsk_rx_channels",
            "qpsk_rx_frames", "qpsk_rx_batch", "qpsk_rx_batch_device", "qpsk_strerror",
            "cnormf", "qpsk_mod", "qpsk_demod", "qpsk_rx_frame", "qpsk_tx_frame",
            "qpsk_rx_init", "qpsk_tx_init", "qpsk_surface_error", "qpsk_tx_state_init",
@@ -127,20 +130,27 @@ def _ptr(a) -> int | None:
     return a.data_ptr()  # torch tensor (device memory)
 
 
+# receiver semantics (include/qpsk_batch.h QPSK_MODE_*)
+MODE_REFERENCE = 0   # bit-identical to the reference as built
+MODE_DEC752 = 1      # decimated_frame[752] ("intended semantics"), NOT reference parity
+
+
 class Receiver:
     """A batch of ``nch`` independent receivers on one GPU (``qpsk_ctx``).
 
     Each channel behaves like the reference receiver fed that channel's stream
     from a fresh start (src/qpsk.c:427-458); state persists across calls.
+    ``mode`` selects the receiver semantics (MODE_REFERENCE or MODE_DEC752).
     """
 
-    def __init__(self, nch: int, device: int = 0):
+    def __init__(self, nch: int, device: int = 0, mode: int = MODE_REFERENCE):
         err = C.c_int(0)
-        self._h = lib().qpsk_rx_create(device, nch, C.byref(err))
+        self._h = lib().qpsk_rx_create_mode(device, nch, mode, C.byref(err))
         if not self._h:
             _check(err.value or -3)
         self.nch = nch
         self.device = device
+        self.mode = int(lib().qpsk_rx_mode(self._h))
 
     def close(self) -> None:
         if getattr(self, "_h", None):

@@ -26,6 +26,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <utility>
+
 #include "qpsk_batch.h"
 #include "qpsk_consts.h"
 #include "qpsk_hunt.h"
@@ -41,11 +43,24 @@ namespace {
 // (256 channels per CU), smaller ones spread over more CUs with G = 2 or 1.
 constexpr int kMaxGroups = 4;
 constexpr int kWinStride = 168;        // window row: slot k+1 = dec[mi+k], 84 float4
-// front LDS (float2 units): M = m_{n-2}[1832..1879] ++ m_{n-1}[0..1191]   (1240)
-//                            ++ m_{n-1}[1832..1879] ++ m_n[0..103]        (152)
-// TU (255 correlator terms, permuted) reuses M once the FIR is done.
-constexpr int kM1 = 1240, kM = 1392, kDec = 296;
-constexpr int kItems = kM / 2;         // 696 two-sample (dword) input items
+constexpr int kDec = 296;
+// Receiver semantics (qpsk_batch.h QPSK_MODE_*): 0 = the reference as built
+// (gcc -O2 "model A" decimated_frame overflow); 1 = dec752, the
+// array with the 752 entries its loop writes (NOT
+// reference parity).  Only the front wave's inputs and FIR differ.
+//
+// front LDS (float2 units), MODE 0:
+//   M = m_{n-2}[1832..1879] ++ m_{n-1}[0..1191]   (1240)  -> D_n[0..187]
+//    ++ m_{n-1}[1832..1879] ++ m_n[0..103]        (152)   -> F_{n+1}[0..101]
+// MODE 1:
+//   M = m_{n-2}[1832..1879] ++ m_{n-1}[0..1701]   (1750)  -> D_n[0..289]
+// TU (255 correlator terms, permuted) reuses M once the FIR is done.  MODE 1
+// keeps one dec buffer per front wave (LDS budget); the previous channel's
+// window is read from it before the FIR overwrites it (same wave, in order).
+constexpr int kM1 = 1240;
+template <int MODE> struct Cfg;
+template <> struct Cfg<0> { static constexpr int kM = 1392, kDecBuf = 2; };
+template <> struct Cfg<1> { static constexpr int kM = 1750, kDecBuf = 1; };
 
 // (re, im) pairs as 2-wide vectors: a complex add / complex*real product is one
 // packed fp32 instruction (v_pk_add_f32 / v_pk_mul_f32: IEEE per lane, no
@@ -114,11 +129,15 @@ __device__ __forceinline__ const int16_t* frame_ptr(const RxArgs& a, int ch, int
 }
 
 // ---------------------------------------------------------------- front wave
-// Input of one channel for frame n: 696 two-sample items d, item d -> M[2d..2d+1]:
+// Input of one channel for frame n: kM/2 two-sample items d, item d -> M[2d..2d+1]:
+// MODE 0 (696 items):
 //   d <  24 : x_{n-2}[1832 + 2d]          d < 620 : x_{n-1}[2(d-24)]
 //   d < 644 : x_{n-1}[1832 + 2(d-620)]    d < 696 : x_n[2(d-644)]
-// Lane l owns items l + 64i, i < 11; i is a compile-time constant below.
-constexpr int kPf = (kItems + 63) / 64;   // 11 prefetched dwords per lane
+// MODE 1 (875 items):
+//   d <  24 : x_{n-2}[1832 + 2d]          d < 875 : x_{n-1}[2(d-24)]
+// Lane l owns items l + 64i, i < kPf; i is a compile-time constant below.
+template <int MODE> constexpr int kItems = Cfg<MODE>::kM / 2;
+template <int MODE> constexpr int kPf = (kItems<MODE> + 63) / 64;   // 11 / 14 dwords per lane
 
 struct Src {
     const int16_t* xm2;
@@ -131,7 +150,7 @@ __device__ __forceinline__ Src srcs(const RxArgs& a, int ch, int n) {
 }
 
 // which frame (0: x_{n-2}, 1: x_{n-1}, 2: x_n; -1: none) and sample index of item l + 64i
-template <int i>
+template <int MODE, int i>
 __device__ __forceinline__ int item(int lane, int& t) {
     const int d = lane + 64 * i;
     if (i == 0) {
@@ -139,42 +158,53 @@ __device__ __forceinline__ int item(int lane, int& t) {
         t = 2 * (lane - 24);
         return 1;
     }
+    if (MODE == 1) {
+        if (d < kItems<1>) { t = 2 * (d - 24); return 1; }
+        t = 0;
+        return -1;
+    }
     if (i < 9) { t = 2 * (d - 24); return 1; }
     if (i == 9) { t = d < 620 ? 2 * (d - 24) : 1832 + 2 * (d - 620); return 1; }
     if (d < 644) { t = 1832 + 2 * (d - 620); return 1; }
-    if (d < kItems) { t = 2 * (d - 644); return 2; }
+    if (d < kItems<0>) { t = 2 * (d - 644); return 2; }
     t = 0;
     return -1;
 }
 
-template <int i>
+template <int MODE, int i>
 __device__ __forceinline__ void load_item(const Src& s, int lane, int& r) {
     int t;
-    const int f = item<i>(lane, t);
+    const int f = item<MODE, i>(lane, t);
     if (f >= 0) r = *reinterpret_cast<const int*>((f == 0 ? s.xm2 : f == 1 ? s.xm1 : s.x0) + t);
 }
 
-__device__ __forceinline__ void prefetch(const Src& s, int lane, int (&r)[kPf]) {
-    load_item<0>(s, lane, r[0]); load_item<1>(s, lane, r[1]); load_item<2>(s, lane, r[2]);
-    load_item<3>(s, lane, r[3]); load_item<4>(s, lane, r[4]); load_item<5>(s, lane, r[5]);
-    load_item<6>(s, lane, r[6]); load_item<7>(s, lane, r[7]); load_item<8>(s, lane, r[8]);
-    load_item<9>(s, lane, r[9]); load_item<10>(s, lane, r[10]);
+template <int MODE, int... I>
+__device__ __forceinline__ void prefetch_seq(const Src& s, int lane, int (&r)[kPf<MODE>],
+                                             std::integer_sequence<int, I...>) {
+    (load_item<MODE, I>(s, lane, r[I]), ...);
+}
+
+template <int MODE>
+__device__ __forceinline__ void prefetch(const Src& s, int lane, int (&r)[kPf<MODE>]) {
+    prefetch_seq<MODE>(s, lane, r, std::make_integer_sequence<int, kPf<MODE>>{});
 }
 
 // src/qpsk.c:139-144 as (-1)^G * P[t] * (x * 2^-14), two samples per item.
 // NO: frame g-1 (f == 1) is the negated one (then g-2 and g are not).  Items
-// 1..9 hold frame g-1 in every lane, so their sign is a compile-time negation
-// (a free source modifier); items 0 and 10 straddle two frames per lane.
-template <int i, bool NO>
+// 1..9 (MODE 0) / 1..13 (MODE 1) hold frame g-1 in every lane, so their sign is
+// a compile-time negation (a free source modifier); items 0 and 10 (MODE 0)
+// straddle two frames per lane.
+template <int MODE, int i, bool NO>
 __device__ __forceinline__ void mix_item(int lane, int r, const float2* P, float2* M) {
     int t;
-    const int f = item<i>(lane, t);
+    const int f = item<MODE, i>(lane, t);
     if (f < 0) return;
     const float4 p = *reinterpret_cast<const float4*>(P + t);
     const float v0 = (float)(int16_t)(r & 0xffff);
     const float v1 = (float)(int16_t)(r >> 16);
     float4 o;
-    if (i >= 1 && i <= 9) {
+    constexpr bool kAllPrev = MODE == 1 ? i >= 1 : (i >= 1 && i <= 9);
+    if (kAllPrev) {
         o = NO ? make_float4((-p.x) * v0, (-p.y) * v0, (-p.z) * v1, (-p.w) * v1)
                : make_float4(p.x * v0, p.y * v0, p.z * v1, p.w * v1);
     } else {
@@ -184,20 +214,18 @@ __device__ __forceinline__ void mix_item(int lane, int r, const float2* P, float
     *reinterpret_cast<float4*>(M + 2 * (lane + 64 * i)) = o;
 }
 
-template <bool NO>
-__device__ __forceinline__ void mix_all(int lane, const int (&r)[kPf], const float2* P, float2* M) {
-    mix_item<0, NO>(lane, r[0], P, M); mix_item<1, NO>(lane, r[1], P, M);
-    mix_item<2, NO>(lane, r[2], P, M); mix_item<3, NO>(lane, r[3], P, M);
-    mix_item<4, NO>(lane, r[4], P, M); mix_item<5, NO>(lane, r[5], P, M);
-    mix_item<6, NO>(lane, r[6], P, M); mix_item<7, NO>(lane, r[7], P, M);
-    mix_item<8, NO>(lane, r[8], P, M); mix_item<9, NO>(lane, r[9], P, M);
-    mix_item<10, NO>(lane, r[10], P, M);
+template <int MODE, bool NO, int... I>
+__device__ __forceinline__ void mix_seq(int lane, const int (&r)[kPf<MODE>], const float2* P,
+                                        float2* M, std::integer_sequence<int, I...>) {
+    (mix_item<MODE, I, NO>(lane, r[I], P, M), ...);
 }
 
-__device__ __forceinline__ void mix(int lane, const int (&r)[kPf], unsigned g, const float2* P,
-                                    float2* M) {
-    if (((g - 1u) & 1u) != 0) mix_all<true>(lane, r, P, M);   // frame g-1 odd
-    else mix_all<false>(lane, r, P, M);
+template <int MODE>
+__device__ __forceinline__ void mix(int lane, const int (&r)[kPf<MODE>], unsigned g,
+                                    const float2* P, float2* M) {
+    constexpr auto kSeq = std::make_integer_sequence<int, kPf<MODE>>{};
+    if (((g - 1u) & 1u) != 0) mix_seq<MODE, true>(lane, r, P, M, kSeq);   // frame g-1 odd
+    else mix_seq<MODE, false>(lane, r, P, M, kSeq);
 }
 
 // max over the 64 lanes of a wave (DPP row shifts / row broadcasts, no LDS trips)
@@ -230,11 +258,49 @@ __device__ __forceinline__ f2 ld2nt(const float2* p) {
 #define FACC_PARAM
 #define FACC_ARG
 #endif
+// MODE 1 (dec752): dec_{n+1} = D_n[0..289] only; lane l makes D[5l .. 5l+4]
+// from the 69 samples M[25l + rt + s] (58 lanes: 290 outputs, 490 packed
+// instructions per channel like MODE 0's 188 + 102).  Lane stride 25 float2
+// = 50 dwords (odd multiple of 2): the b64 reads of 32 lanes cover the 64
+// banks once.
+__device__ __forceinline__ void fir_dec752(int lane, int rt, const float2* M, float2* dec) {
+    if (lane < QK_NDECOBS / 5) {
+        const float2* b = M + 25 * lane + rt;
+        f2 y[5] = {{0.0f, 0.0f}, {0.0f, 0.0f}, {0.0f, 0.0f}, {0.0f, 0.0f}, {0.0f, 0.0f}};
+#pragma unroll
+        for (int s0 = 0; s0 < 69; s0 += 15) {
+            f2 v[15];
+#pragma unroll
+            for (int j = 0; j < 15; j++)
+                if (s0 + j < 69) v[j] = ld2nt(b + s0 + j);
+#pragma unroll
+            for (int j = 0; j < 15; j++) {
+                const int s = s0 + j;
+#pragma unroll
+                for (int m = 0; m < 5; m++) {
+                    const int k = s - 5 * m;
+                    if (s < 69 && k >= 0 && k < QK_NTAPS) y[m] = y[m] + v[j] * QK_RRC[k];
+                }
+            }
+        }
+#pragma unroll
+        for (int m = 0; m < 5; m++) {
+            const f2 o = y[m] * QK_GAIN;
+            dec[5 * lane + m] = make_float2(o.x, o.y);
+        }
+    }
+}
+
+template <int MODE>
 __device__ __forceinline__ int front_channel(int lane, int rt, float2* M, float2* dec,
                                              const float* BT FACC_PARAM) {
 #ifdef QPSK_STAMPS
     unsigned long long ft0 = stamp_now();
 #endif
+    if constexpr (MODE == 1) {
+        fir_dec752(lane, rt, M, dec);
+        FSTAMP(0);
+    } else {
     // RRC (src/fir.c:36-42), outputs accumulated in tap order.  Decimated
     // outputs D[o] = fir_out[5o + rt] (model A): lane l makes
     // o = 3l..3l+2 from the 59 samples M[15l + rt + s], read in batches.
@@ -289,6 +355,7 @@ __device__ __forceinline__ int front_channel(int lane, int rt, float2* M, float2
             const f2 o = y[m] * QK_GAIN;
             dec[QK_NDEC + 2 * lane + m] = make_float2(o.x, o.y);
         }
+    }
     }
     wave_lds_sync();
     FSTAMP(1);
@@ -687,7 +754,7 @@ __global__ void __launch_bounds__(256) rx_data_kernel(const float4* jobs, unsign
 // pointer is a global-memory pointer (global_load/store, no flat) and nothing of
 // the argument block is indexed dynamically (no scratch copy).
 // 12 waves per workgroup, 3 per SIMD (<= 168 VGPRs), one workgroup per CU (LDS).
-template <int G, int FP>
+template <int G, int FP, int MODE>
 __global__ void __launch_bounds__(64 * G * (1 + FP), 3) rx_kernel(
     const int16_t* in, int16_t* hist, const float2* ptab, const unsigned long long* ks,
     float2* win0, float2* win1, int* mi0, int* mi1, int* rt0, int* rt1, uint8_t* bits,
@@ -700,8 +767,9 @@ __global__ void __launch_bounds__(64 * G * (1 + FP), 3) rx_kernel(
     const RxArgs a{in, hist, ptab, ks, win0, win1, mi0, mi1, rt0, rt1, bits, valid, trace, soft,
                    jobs, njobs, nch, F, g0, roles};
     __shared__ __attribute__((aligned(16))) float2 P[QK_FRAME];
+    constexpr int kM = Cfg<MODE>::kM, kDecBuf = Cfg<MODE>::kDecBuf;
     __shared__ __attribute__((aligned(16))) float2 Ms[kFrontWaves][kM];
-    __shared__ __attribute__((aligned(16))) float2 decs[kFrontWaves][2][kDec];
+    __shared__ __attribute__((aligned(16))) float2 decs[kFrontWaves][kDecBuf][kDec];
     __shared__ int mi_s[kGroups][2][QK_GROUP], rt_s[kGroups][2][QK_GROUP];
     __shared__ __attribute__((aligned(16))) float BT[qhunt::kBT];   // correlator's B
     const int lane = threadIdx.x & 63;
@@ -756,10 +824,10 @@ __global__ void __launch_bounds__(64 * G * (1 + FP), 3) rx_kernel(
         const int ch0 = (grp0 + gi) * QK_GROUP + cbeg;
         const int nlive = max(0, min(kFrontCh, a.nch - ch0));
         float2* M = Ms[f];
-        int pf[kPf];
+        int pf[kPf<MODE>];
         const bool on = (a.roles & 2) != 0 && nlive > 0;
         if (((a.roles >> 4) & 3) == 1) __builtin_amdgcn_s_setprio(2);
-        if (on) prefetch(srcs(a, ch0, 0), lane, pf);
+        if (on) prefetch<MODE>(srcs(a, ch0, 0), lane, pf);
         STAMP_DECL
         for (int n = 0; n < a.F; n++) {
             const int p = n & 1;
@@ -768,18 +836,18 @@ __global__ void __launch_bounds__(64 * G * (1 + FP), 3) rx_kernel(
             int pmi = 0;
             for (int c = 0; on && c < nlive; c++) {
                 const int ch = ch0 + c;
-                float2* dcur = decs[f][c & 1];
-                mix(lane, pf, g, P, M);
+                float2* dcur = decs[f][c % kDecBuf];
+                mix<MODE>(lane, pf, g, P, M);
                 STAMP(0);
-                if (c > 0) store_window(lane, pmi, decs[f][(c - 1) & 1], wout + (size_t)(ch - 1) * kWinStride);
+                if (c > 0) store_window(lane, pmi, decs[f][(c - 1) % kDecBuf], wout + (size_t)(ch - 1) * kWinStride);
                 {   // next channel of this frame, else the first of the next frame
                     const bool same = c + 1 < nlive;
                     if (same || n + 1 < a.F)
-                        prefetch(srcs(a, same ? ch + 1 : ch0, same ? n : n + 1), lane, pf);
+                        prefetch<MODE>(srcs(a, same ? ch + 1 : ch0, same ? n : n + 1), lane, pf);
                 }
                 wave_lds_sync();
                 STAMP(1);
-                pmi = front_channel(lane, rt_s[gi][p][cbeg + c], M, dcur, BT FACC_ARG);
+                pmi = front_channel<MODE>(lane, rt_s[gi][p][cbeg + c], M, dcur, BT FACC_ARG);
                 if (lane == 0) mi_s[gi][p ^ 1][cbeg + c] = pmi;
                 if (c + 1 == nlive) store_window(lane, pmi, dcur, wout + (size_t)ch * kWinStride);
                 wave_lds_sync();
@@ -789,8 +857,9 @@ __global__ void __launch_bounds__(64 * G * (1 + FP), 3) rx_kernel(
             STAMP(7);
         }
         STAMP_FLUSH();
-        // carry the samples the next call needs: x_{F-1}[0..1191], x_{F-1}[1832..1879],
-        // x_{F-2}[1832..1879]
+        // carry the samples the next call needs: x_{F-1}[0..hi), x_{F-1}[1832..1879],
+        // x_{F-2}[1832..1879]; hi = 1192 (MODE 0) or 1704 (MODE 1), in 8-sample units
+        constexpr int kHead8 = MODE == 1 ? 213 : 149;
         for (int c = 0; c < nlive; c++) {
             const int ch = ch0 + c;
             int16_t* h0 = a.hist + (size_t)ch * 2 * QK_FRAME;
@@ -801,8 +870,8 @@ __global__ void __launch_bounds__(64 * G * (1 + FP), 3) rx_kernel(
                 const int t = 1832 + 8 * lane;
                 *reinterpret_cast<int4*>(h0 + t) = *reinterpret_cast<const int4*>(prev + t);
             }
-            for (int u = lane; u < 155; u += 64) {
-                const int t = u < 149 ? 8 * u : 1832 + 8 * (u - 149);
+            for (int u = lane; u < kHead8 + 6; u += 64) {
+                const int t = u < kHead8 ? 8 * u : 1832 + 8 * (u - kHead8);
                 *reinterpret_cast<int4*>(h1 + t) = *reinterpret_cast<const int4*>(last + t);
             }
         }
@@ -821,6 +890,7 @@ float bits2f(uint32_t u) {
 
 struct qpsk_ctx {
     int device = 0, nch = 0, ngroup = 0;
+    int mode = QPSK_MODE_REFERENCE;   // receiver semantics, fixed at creation
     uint64_t frames = 0;
     hipStream_t stream = nullptr;
     float2* d_ptab = nullptr;
@@ -951,9 +1021,16 @@ static void ctx_free(qpsk_ctx* c) {
 }
 
 extern "C" qpsk_ctx* qpsk_rx_create(int device, int nch, int* err) {
+    return qpsk_rx_create_mode(device, nch, QPSK_MODE_REFERENCE, err);
+}
+
+extern "C" qpsk_ctx* qpsk_rx_create_mode(int device, int nch, int mode, int* err) {
     int dummy;
     if (!err) err = &dummy;
-    if (nch < 1) { *err = QPSK_EINVAL; return nullptr; }
+    if (nch < 1 || (mode != QPSK_MODE_REFERENCE && mode != QPSK_MODE_DEC752)) {
+        *err = QPSK_EINVAL;
+        return nullptr;
+    }
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) {
         *err = QPSK_ENODEV;
@@ -963,6 +1040,7 @@ extern "C" qpsk_ctx* qpsk_rx_create(int device, int nch, int* err) {
     if (!c) { *err = QPSK_ENOMEM; return nullptr; }
     c->device = device;
     c->nch = nch;
+    c->mode = mode;
     c->ngroup = (nch + QK_GROUP - 1) / QK_GROUP;
     if (const char* ab = getenv("QPSK_ABLATE")) {   // timing experiments; output invalid
         if (!strcmp(ab, "front")) c->roles = (c->roles & ~3) | 2;
@@ -1011,6 +1089,7 @@ extern "C" void qpsk_rx_destroy(qpsk_ctx* c) {
 }
 
 extern "C" int qpsk_rx_channels(const qpsk_ctx* c) { return c ? c->nch : 0; }
+extern "C" int qpsk_rx_mode(const qpsk_ctx* c) { return c ? c->mode : QPSK_EINVAL; }
 extern "C" uint64_t qpsk_rx_frames(const qpsk_ctx* c) { return c ? c->frames : 0; }
 
 // rx_data_kernel grid: persistent, 4 workgroups of 256 per CU
@@ -1055,16 +1134,22 @@ extern "C" int qpsk_rx_batch_device(qpsk_ctx* c, const int16_t* d_in, int F, uin
     // batch in one wave of workgroups (QPSK_SHAPE=4x2|2x4|1x8 overrides)
     const int G = c->shape_groups > 0 ? c->shape_groups
                 : c->ngroup <= c->ncu ? 1 : c->ngroup <= 2 * c->ncu ? 2 : 4;
-#define QPSK_LAUNCH(GG, FF)                                                                    \
-    hipLaunchKernelGGL((rx_kernel<GG, FF>), dim3((c->ngroup + GG - 1) / GG),                  \
+#define QPSK_LAUNCH(GG, FF, MM)                                                                \
+    hipLaunchKernelGGL((rx_kernel<GG, FF, MM>), dim3((c->ngroup + GG - 1) / GG),              \
                        dim3(64 * GG * (1 + FF)), 0, s, d_in, c->d_hist, c->d_ptab, c->d_ks,    \
                        c->d_win[0], c->d_win[1], c->d_mi[0], c->d_mi[1], c->d_rt[0], c->d_rt[1], \
                        d_bits, d_valid, d_trace, reinterpret_cast<float2*>(d_soft), c->d_jobs,  \
                        c->d_njobs + parity, c->nch, F, (unsigned)(c->frames & 0xffffffffu),     \
                        c->roles)
-    if (G == 1) QPSK_LAUNCH(1, 8);
-    else if (G == 2) QPSK_LAUNCH(2, 4);
-    else QPSK_LAUNCH(4, 2);
+    if (c->mode == QPSK_MODE_DEC752) {
+        if (G == 1) QPSK_LAUNCH(1, 8, 1);
+        else if (G == 2) QPSK_LAUNCH(2, 4, 1);
+        else QPSK_LAUNCH(4, 2, 1);
+    } else {
+        if (G == 1) QPSK_LAUNCH(1, 8, 0);
+        else if (G == 2) QPSK_LAUNCH(2, 4, 0);
+        else QPSK_LAUNCH(4, 2, 0);
+    }
 #undef QPSK_LAUNCH
     HCHECK(hipGetLastError());
     if (slot >= 0) HCHECK(hipEventRecord(c->ev[slot][1], s));

@@ -116,3 +116,14 @@ def test_record_writer_reproduces_reference_output_file(golden_dir):
     assert len(recs) == exp["output_bytes"] == 496 * int(valid.sum())
     assert hashlib.md5(recs).hexdigest() == exp["output_md5"]
     assert sc.records(bits, np.zeros(nf, np.uint8)) == b""
+
+
+def test_create_mode_rejects_unknown_modes():
+    """qpsk_rx_create_mode validates its arguments before touching a device."""
+    import ctypes as C
+    L = sc.lib()
+    for mode, nch in ((2, 4), (-1, 4), (sc.MODE_DEC752, 0)):
+        err = C.c_int(0)
+        assert not L.qpsk_rx_create_mode(0, nch, mode, C.byref(err))
+        assert err.value == -1   # QPSK_EINVAL
+    assert L.qpsk_rx_mode(None) == -1
