@@ -123,6 +123,35 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Dual-chain kernel (rx_kernel<.., DUAL = true>): per-frame progress counters
+// in LDS instead of a workgroup barrier.  Every wave of the (single) workgroup
+// is resident, and every counter is advanced by every frame of its producer,
+// so each wait ends; the bound only turns a logic error into wrong output
+// instead of a hung GPU.
+__device__ __forceinline__ void spin_wait(int* p, int v) {
+    for (unsigned it = 0; it < (1u << 22); it++) {   // ~0.1 s; a frame is ~2.5k spins
+        const int c = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+        if (c >= v) break;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// publish: every earlier store of this wave (LDS and global) is visible to the
+// workgroup before the counter moves
+__device__ __forceinline__ void signal_set(int* p, int v, int lane) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+__device__ __forceinline__ void signal_add(int* p, int v, int lane) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 __device__ __forceinline__ const int16_t* frame_ptr(const RxArgs& a, int ch, int k) {
     return k >= 0 ? a.in + ((size_t)ch * a.F + k) * QK_FRAME
                   : a.hist + ((size_t)ch * 2 + (k + 2)) * QK_FRAME;
@@ -401,6 +430,28 @@ __device__ __forceinline__ void store_window(int lane, int mi, const float2* dec
     }
 }
 
+// carry the samples the next call needs: x_{F-1}[0..hi), x_{F-1}[1832..1879],
+// x_{F-2}[1832..1879]; hi = 1192 (MODE 0) or 1704 (MODE 1), in 8-sample units
+template <int MODE>
+__device__ __forceinline__ void carry_history(const int16_t* in, int16_t* hist, int F, int ch0, int nlive, int lane) {
+    constexpr int kHead8 = MODE == 1 ? 213 : 149;
+    for (int c = 0; c < nlive; c++) {
+        const int ch = ch0 + c;
+        int16_t* h0 = hist + (size_t)ch * 2 * QK_FRAME;
+        int16_t* h1 = h0 + QK_FRAME;
+        const int16_t* last = F >= 1 ? in + ((size_t)ch * F + (F - 1)) * QK_FRAME : h1;
+        const int16_t* prev = F >= 2 ? in + ((size_t)ch * F + (F - 2)) * QK_FRAME : h1;
+        if (lane < 6) {   // F == 1: prev is h1; its load completes before the h1 stores
+            const int t = 1832 + 8 * lane;
+            *reinterpret_cast<int4*>(h0 + t) = *reinterpret_cast<const int4*>(prev + t);
+        }
+        for (int u = lane; u < kHead8 + 6; u += 64) {
+            const int t = u < kHead8 ? 8 * u : 1832 + 8 * (u - kHead8);
+            *reinterpret_cast<int4*>(h1 + t) = *reinterpret_cast<const int4*>(last + t);
+        }
+    }
+}
+
 // ---------------------------------------------------------------- back role
 // Complex values are f2 = (re, im).  cmul(A, C) = (ac - bd, ad + bc) with every
 // product and the final sum/difference rounded once, exactly as gcc expands
@@ -632,8 +683,11 @@ __device__ __forceinline__ int train(Kal& k, f2 (&x)[5], const f2* wp2, bool& ba
 
 // One frame of the back wave: lane = channel.  Window slots 1..163 hold
 // dec[mi .. mi+162]; read two slots (16 B) every two steps.
+// get_rt() yields rx_timing of frame n; it is called only after the training,
+// so the dual-chain kernel can wait for the previous frame's decision there.
+template <typename RtFn>
 __device__ __forceinline__ void back_frame(const RxArgs& a, int ch, bool live, int n, int mi,
-                                           int rt, const float2* win, int* rt_next) {
+                                           RtFn get_rt, const float2* win, int* rt_next) {
     const float4* wp = reinterpret_cast<const float4*>(win);
     Kal k = kal_reset();
     f2 x[5];
@@ -674,6 +728,7 @@ __device__ __forceinline__ void back_frame(const RxArgs& a, int ch, bool live, i
             for (int ss = 0; ss < QK_NDSYM; ss++) so[ss] = make_float2(0.0f, 0.0f);
         }
     }
+    const int rt = get_rt();
     const int rtn = valid ? mi + QK_NPRE : rt;    // src/qpsk.c:219
     *rt_next = rtn;
     if (live) {
@@ -754,16 +809,33 @@ __global__ void __launch_bounds__(256) rx_data_kernel(const float4* jobs, unsign
 // pointer is a global-memory pointer (global_load/store, no flat) and nothing of
 // the argument block is indexed dynamically (no scratch copy).
 // 12 waves per workgroup, 3 per SIMD (<= 168 VGPRs), one workgroup per CU (LDS).
-template <int G, int FP, int MODE>
-__global__ void __launch_bounds__(64 * G * (1 + FP), 3) rx_kernel(
+//
+// DUAL (G == 1 only): two back waves, one for the even and one for the odd
+// frames of the call.  Frame n's training needs only frame n-1's front, and
+// frame n-1's front needs frame n-2's decision, so consecutive frames' training
+// is independent: the back of frame n+1 starts as soon as the front of frame n
+// is done, while the back of frame n is still running.  The per-frame time
+// drops from max(back, front) to (back + front) / 2 where one serial back wave
+// per CU bounds the kernel (<= 16,384 channels per GPU).  Progress is handed
+// over through LDS counters (bseq: frames decided per back wave; fcnt: front
+// frames finished, by frame parity) instead of __syncthreads().
+//
+// W (DUAL only): channels per group, 64, 32 or 16.  A narrower group leaves
+// back lanes idle but spreads a small batch over more CUs and gives each front
+// wave fewer channels per frame, which shortens the front half of the chain.
+template <int G, int FP, int MODE, bool DUAL, int W = QK_GROUP>
+__global__ void __launch_bounds__(64 * G * ((DUAL ? 2 : 1) + FP), 3) rx_kernel(
     const int16_t* in, int16_t* hist, const float2* ptab, const unsigned long long* ks,
     float2* win0, float2* win1, int* mi0, int* mi1, int* rt0, int* rt1, uint8_t* bits,
     uint8_t* valid, int32_t* trace, float2* soft, float4* jobs, unsigned* njobs, int nch, int F,
     unsigned g0, int roles) {
+    static_assert(!DUAL || G == 1, "dual-chain backs: one group per workgroup");
+    static_assert(W == QK_GROUP || (DUAL && W % FP == 0 && W <= QK_GROUP), "group width");
     constexpr int kGroups = G, kFrontPer = FP;
-    constexpr int kFrontCh = QK_GROUP / kFrontPer;     // channels per front wave
+    constexpr int kBackWaves = DUAL ? 2 : kGroups;
+    constexpr int kFrontCh = W / kFrontPer;            // channels per front wave
     constexpr int kFrontWaves = kGroups * kFrontPer;
-    constexpr int kBlock = 64 * (kGroups + kFrontWaves);
+    constexpr int kBlock = 64 * (kBackWaves + kFrontWaves);
     const RxArgs a{in, hist, ptab, ks, win0, win1, mi0, mi1, rt0, rt1, bits, valid, trace, soft,
                    jobs, njobs, nch, F, g0, roles};
     __shared__ __attribute__((aligned(16))) float2 P[QK_FRAME];
@@ -772,6 +844,7 @@ __global__ void __launch_bounds__(64 * G * (1 + FP), 3) rx_kernel(
     __shared__ __attribute__((aligned(16))) float2 decs[kFrontWaves][kDecBuf][kDec];
     __shared__ int mi_s[kGroups][2][QK_GROUP], rt_s[kGroups][2][QK_GROUP];
     __shared__ __attribute__((aligned(16))) float BT[qhunt::kBT];   // correlator's B
+    __shared__ int bseq[2], fcnt[2];   // DUAL progress counters
     const int lane = threadIdx.x & 63;
     // wave-uniform by construction; readfirstlane tells the compiler, so every
     // per-wave index and pointer below lives in SGPRs
@@ -781,13 +854,82 @@ __global__ void __launch_bounds__(64 * G * (1 + FP), 3) rx_kernel(
         reinterpret_cast<float4*>(P)[i] = reinterpret_cast<const float4*>(a.ptab)[i];
     qhunt::bconst_lds(threadIdx.x, kBlock, BT);
     if (wave < kGroups) {   // per-channel state of the groups at the call's first frame
-        const int ch = (grp0 + wave) * QK_GROUP + lane;
-        if (ch < a.nch) {
+        const int ch = (grp0 + wave) * W + lane;
+        if (lane < W && ch < a.nch) {
             mi_s[wave][0][lane] = mi_of(a, a.g0)[ch];
             rt_s[wave][0][lane] = rt_of(a, a.g0)[ch];
         }
     }
+    if (threadIdx.x < 2) bseq[threadIdx.x] = fcnt[threadIdx.x] = 0;
     __syncthreads();
+    if constexpr (DUAL) {
+        if (wave < kBackWaves) {
+            // ---------------------------------------------------- back, frames n = wave mod 2
+            const int ch = grp0 * W + lane;
+            const bool live = lane < W && ch < a.nch;
+            if (((a.roles >> 4) & 3) == 2) __builtin_amdgcn_s_setprio(2);
+            for (int n = wave; n < a.F; n += 2) {
+                const int p = n & 1;
+                // front(n-1) done by every front wave: window n and mi_n are in place
+                if (n > 0) spin_wait(&fcnt[p ^ 1], kFrontWaves * ((n - 1) / 2 + 1));
+                back_frame(a, live ? ch : 0, live, n, mi_s[0][p][lane],
+                           [&] {   // rx_timing of frame n = the decision of frame n-1
+                               if (n > 0) spin_wait(&bseq[p ^ 1], n);
+                               return rt_s[0][p][lane];
+                           },
+                           win_of(a, a.g0 + (unsigned)n) + (size_t)(live ? ch : 0) * kWinStride,
+                           &rt_s[0][p ^ 1][lane]);
+                signal_set(&bseq[p], n + 1, lane);
+            }
+        } else {
+            // ---------------------------------------------------- front
+            const int f = wave - kBackWaves;
+            const int cbeg = f * kFrontCh;
+            const int ch0 = grp0 * W + cbeg;
+            const int nlive = max(0, min(kFrontCh, a.nch - ch0));
+            float2* M = Ms[f];
+            int pf[kPf<MODE>];
+            if (((a.roles >> 4) & 3) == 1) __builtin_amdgcn_s_setprio(2);
+            if (nlive > 0) prefetch<MODE>(srcs(a, ch0, 0), lane, pf);
+            for (int n = 0; n < a.F; n++) {
+                const int p = n & 1;
+                const unsigned g = a.g0 + (unsigned)n;
+                float2* wout = win_of(a, g + 1u);
+                // back(n-1) done: rx_timing of frame n, and window n+1's buffer
+                // (window n-1) and mi_s[p ^ 1] (mi_{n-1}) are free
+                if (n > 0) spin_wait(&bseq[p ^ 1], n);
+                int pmi = 0;
+                for (int c = 0; c < nlive; c++) {
+                    const int ch = ch0 + c;
+                    float2* dcur = decs[f][c % kDecBuf];
+                    mix<MODE>(lane, pf, g, P, M);
+                    if (c > 0) store_window(lane, pmi, decs[f][(c - 1) % kDecBuf], wout + (size_t)(ch - 1) * kWinStride);
+                    {
+                        const bool same = c + 1 < nlive;
+                        if (same || n + 1 < a.F)
+                            prefetch<MODE>(srcs(a, same ? ch + 1 : ch0, same ? n : n + 1), lane, pf);
+                    }
+                    wave_lds_sync();
+                    pmi = front_channel<MODE>(lane, rt_s[0][p][cbeg + c], M, dcur, BT);
+                    if (lane == 0) mi_s[0][p ^ 1][cbeg + c] = pmi;
+                    if (c + 1 == nlive) store_window(lane, pmi, dcur, wout + (size_t)ch * kWinStride);
+                    wave_lds_sync();
+                }
+                signal_add(&fcnt[p], 1, lane);
+            }
+            carry_history<MODE>(a.in, a.hist, a.F, ch0, nlive, lane);
+        }
+        __syncthreads();
+        if (wave == 0) {   // per-channel state after the call's last frame
+            const int ch = grp0 * W + lane;
+            if (lane < W && ch < a.nch) {
+                const unsigned ge = a.g0 + (unsigned)a.F;
+                mi_of(a, ge)[ch] = mi_s[0][a.F & 1][lane];
+                rt_of(a, ge)[ch] = rt_s[0][a.F & 1][lane];
+            }
+        }
+        return;
+    }
     if (wave < kGroups) {
         // ------------------------------------------------------------ back
         const int gi = wave;
@@ -798,10 +940,12 @@ __global__ void __launch_bounds__(64 * G * (1 + FP), 3) rx_kernel(
         STAMP_DECL
         for (int n = 0; n < a.F; n++) {
             const int p = n & 1;
-            if (any && (a.roles & 1))
-                back_frame(a, live ? ch : 0, live, n, mi_s[gi][p][lane], rt_s[gi][p][lane],
+            if (any && (a.roles & 1)) {
+                const int rt = rt_s[gi][p][lane];
+                back_frame(a, live ? ch : 0, live, n, mi_s[gi][p][lane], [=] { return rt; },
                            win_of(a, a.g0 + (unsigned)n) + (size_t)(live ? ch : 0) * kWinStride,
                            &rt_s[gi][p ^ 1][lane]);
+            }
             else
                 rt_s[gi][p ^ 1][lane] = rt_s[gi][p][lane];
             STAMP(13);
@@ -857,24 +1001,7 @@ __global__ void __launch_bounds__(64 * G * (1 + FP), 3) rx_kernel(
             STAMP(7);
         }
         STAMP_FLUSH();
-        // carry the samples the next call needs: x_{F-1}[0..hi), x_{F-1}[1832..1879],
-        // x_{F-2}[1832..1879]; hi = 1192 (MODE 0) or 1704 (MODE 1), in 8-sample units
-        constexpr int kHead8 = MODE == 1 ? 213 : 149;
-        for (int c = 0; c < nlive; c++) {
-            const int ch = ch0 + c;
-            int16_t* h0 = a.hist + (size_t)ch * 2 * QK_FRAME;
-            int16_t* h1 = h0 + QK_FRAME;
-            const int16_t* last = frame_ptr(a, ch, a.F - 1);
-            const int16_t* prev = frame_ptr(a, ch, a.F - 2);
-            if (lane < 6) {   // F == 1: prev is h1; its load completes before the h1 stores
-                const int t = 1832 + 8 * lane;
-                *reinterpret_cast<int4*>(h0 + t) = *reinterpret_cast<const int4*>(prev + t);
-            }
-            for (int u = lane; u < kHead8 + 6; u += 64) {
-                const int t = u < kHead8 ? 8 * u : 1832 + 8 * (u - kHead8);
-                *reinterpret_cast<int4*>(h1 + t) = *reinterpret_cast<const int4*>(last + t);
-            }
-        }
+        carry_history<MODE>(a.in, a.hist, a.F, ch0, nlive, lane);
     }
 }
 
@@ -921,6 +1048,8 @@ struct qpsk_ctx {
     int roles = 3 | (1 << 4);   // roles + priority; QPSK_ABLATE / QPSK_PRIO (profiling)
     int ncu = 256;              // compute units of the device
     int shape_groups = 0;       // 0: by batch size; QPSK_SHAPE (A/B experiments)
+    bool single_back = false;   // QPSK_SHAPE=1x8s: G = 1 without the dual-chain back
+    int width = 0;              // dual-chain group width; 0: by batch size; QPSK_WIDTH
     float pend_ms[2] = {0.0f, 0.0f};
     int pend_frames = 0;
 };
@@ -1051,8 +1180,16 @@ extern "C" qpsk_ctx* qpsk_rx_create_mode(int device, int nch, int mode, int* err
         c->roles = (c->roles & 3) | (v << 4);
     }
     if (getenv("QPSK_FORCE_EXACT")) c->roles |= kForceExact;   // tests: exact-division path
+    if (const char* w = getenv("QPSK_WIDTH")) {
+        const int v = atoi(w);
+        c->width = (v == 16 || v == 32 || v == 64) ? v : 0;
+    }
     if (const char* sh = getenv("QPSK_SHAPE"))
-        c->shape_groups = !strcmp(sh, "1x8") ? 1 : !strcmp(sh, "2x4") ? 2 : !strcmp(sh, "4x2") ? 4 : 0;
+    {
+        c->shape_groups = !strcmp(sh, "1x8") || !strcmp(sh, "1x8s") ? 1
+                        : !strcmp(sh, "2x4") ? 2 : !strcmp(sh, "4x2") ? 4 : 0;
+        c->single_back = !strcmp(sh, "1x8s");
+    }
     int r = herr(hipSetDevice(device));
     if (r == QPSK_OK) {
         int n = 0;
@@ -1134,22 +1271,37 @@ extern "C" int qpsk_rx_batch_device(qpsk_ctx* c, const int16_t* d_in, int F, uin
     // batch in one wave of workgroups (QPSK_SHAPE=4x2|2x4|1x8 overrides)
     const int G = c->shape_groups > 0 ? c->shape_groups
                 : c->ngroup <= c->ncu ? 1 : c->ngroup <= 2 * c->ncu ? 2 : 4;
-#define QPSK_LAUNCH(GG, FF, MM)                                                                \
-    hipLaunchKernelGGL((rx_kernel<GG, FF, MM>), dim3((c->ngroup + GG - 1) / GG),              \
-                       dim3(64 * GG * (1 + FF)), 0, s, d_in, c->d_hist, c->d_ptab, c->d_ks,    \
+#define QPSK_LAUNCH(GG, FF, MM, DD, WW)                                                        \
+    hipLaunchKernelGGL((rx_kernel<GG, FF, MM, DD, WW>),                                        \
+                       dim3((unsigned)((c->nch + (size_t)GG * WW - 1) / ((size_t)GG * WW))),   \
+                       dim3(64 * GG * ((DD ? 2 : 1) + FF)), 0, s, d_in, c->d_hist, c->d_ptab,  \
+                       c->d_ks,                                                                \
                        c->d_win[0], c->d_win[1], c->d_mi[0], c->d_mi[1], c->d_rt[0], c->d_rt[1], \
                        d_bits, d_valid, d_trace, reinterpret_cast<float2*>(d_soft), c->d_jobs,  \
                        c->d_njobs + parity, c->nch, F, (unsigned)(c->frames & 0xffffffffu),     \
                        c->roles)
-    if (c->mode == QPSK_MODE_DEC752) {
-        if (G == 1) QPSK_LAUNCH(1, 8, 1);
-        else if (G == 2) QPSK_LAUNCH(2, 4, 1);
-        else QPSK_LAUNCH(4, 2, 1);
-    } else {
-        if (G == 1) QPSK_LAUNCH(1, 8, 0);
-        else if (G == 2) QPSK_LAUNCH(2, 4, 0);
-        else QPSK_LAUNCH(4, 2, 0);
+    // one group per workgroup: the dual-chain back (DUAL above) unless
+    // QPSK_SHAPE=1x8s forces the single back wave
+    // and the narrowest group width (64/32/16 channels) that still fits the
+    // batch in one wave of workgroups (QPSK_WIDTH overrides)
+    const bool dual = G == 1 && !c->single_back;
+    int W = 64;
+    if (dual) {
+        W = c->width > 0 ? c->width
+          : (size_t)c->nch <= (size_t)16 * c->ncu ? 16 : (size_t)c->nch <= (size_t)32 * c->ncu ? 32 : 64;
     }
+#define QPSK_LAUNCH_MODE(MM)                                                                   \
+    do {                                                                                       \
+        if (dual && W == 16) QPSK_LAUNCH(1, 8, MM, true, 16);                                  \
+        else if (dual && W == 32) QPSK_LAUNCH(1, 8, MM, true, 32);                             \
+        else if (dual) QPSK_LAUNCH(1, 8, MM, true, 64);                                        \
+        else if (G == 1) QPSK_LAUNCH(1, 8, MM, false, 64);                                     \
+        else if (G == 2) QPSK_LAUNCH(2, 4, MM, false, 64);                                     \
+        else QPSK_LAUNCH(4, 2, MM, false, 64);                                                 \
+    } while (0)
+    if (c->mode == QPSK_MODE_DEC752) QPSK_LAUNCH_MODE(1);
+    else QPSK_LAUNCH_MODE(0);
+#undef QPSK_LAUNCH_MODE
 #undef QPSK_LAUNCH
     HCHECK(hipGetLastError());
     if (slot >= 0) HCHECK(hipEventRecord(c->ev[slot][1], s));

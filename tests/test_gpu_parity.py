@@ -213,12 +213,22 @@ def test_c_driver_single_and_batch(golden_dir, tmp_path):
         assert (tmp_path / f"ch{i + 1}.bin").read_bytes() == sc.records(bits[i], valid[i])
 
 
-@pytest.mark.parametrize("shape", ["4x2", "2x4", "1x8"])
+@pytest.mark.parametrize("shape", ["4x2", "2x4", "1x8", "1x8s"])
 def test_every_workgroup_shape(shape, monkeypatch):
     """rx_kernel<G, FP> (groups per workgroup x front waves per group) is chosen
     by batch size; QPSK_SHAPE forces each one on the same ragged batch."""
     monkeypatch.setenv("QPSK_SHAPE", shape)
     x = oracle.synth(61, 300, 12, 5.0)
+    _vs_oracle(x)
+
+
+@pytest.mark.parametrize("width", ["16", "32", "64"])
+def test_dual_chain_group_widths(width, monkeypatch):
+    """One group per workgroup runs the dual-chain kernel (two back waves,
+    even/odd frames, LDS progress counters); QPSK_WIDTH forces its group width
+    (channels per workgroup) on one ragged batch."""
+    monkeypatch.setenv("QPSK_WIDTH", width)
+    x = oracle.synth(64, 333, 15, 4.0)
     _vs_oracle(x)
 
 
