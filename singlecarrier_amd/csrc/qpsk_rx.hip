@@ -57,6 +57,10 @@ constexpr int kDec = 296;
 // TU (255 correlator terms, permuted) reuses M once the FIR is done.  MODE 1
 // keeps one dec buffer per front wave (LDS budget); the previous channel's
 // window is read from it before the FIR overwrites it (same wave, in order).
+#ifndef QPSK_FB
+#define QPSK_FB 15   // FIR samples per LDS batch (A/B knob)
+#endif
+
 constexpr int kM1 = 1240;
 template <int MODE> struct Cfg;
 template <> struct Cfg<0> { static constexpr int kM = 1392, kDecBuf = 2; };
@@ -297,13 +301,13 @@ __device__ __forceinline__ void fir_dec752(int lane, int rt, const float2* M, fl
         const float2* b = M + 25 * lane + rt;
         f2 y[5] = {{0.0f, 0.0f}, {0.0f, 0.0f}, {0.0f, 0.0f}, {0.0f, 0.0f}, {0.0f, 0.0f}};
 #pragma unroll
-        for (int s0 = 0; s0 < 69; s0 += 15) {
-            f2 v[15];
+        for (int s0 = 0; s0 < 69; s0 += QPSK_FB) {
+            f2 v[QPSK_FB];
 #pragma unroll
-            for (int j = 0; j < 15; j++)
+            for (int j = 0; j < QPSK_FB; j++)
                 if (s0 + j < 69) v[j] = ld2nt(b + s0 + j);
 #pragma unroll
-            for (int j = 0; j < 15; j++) {
+            for (int j = 0; j < QPSK_FB; j++) {
                 const int s = s0 + j;
 #pragma unroll
                 for (int m = 0; m < 5; m++) {
@@ -337,13 +341,13 @@ __device__ __forceinline__ int front_channel(int lane, int rt, float2* M, float2
         const float2* b = M + 15 * lane + rt;
         f2 y[3] = {{0.0f, 0.0f}, {0.0f, 0.0f}, {0.0f, 0.0f}};
 #pragma unroll
-        for (int s0 = 0; s0 < 59; s0 += 15) {
-            f2 v[15];
+        for (int s0 = 0; s0 < 59; s0 += QPSK_FB) {
+            f2 v[QPSK_FB];
 #pragma unroll
-            for (int j = 0; j < 15; j++)
+            for (int j = 0; j < QPSK_FB; j++)
                 if (s0 + j < 59) v[j] = ld2nt(b + s0 + j);
 #pragma unroll
-            for (int j = 0; j < 15; j++) {
+            for (int j = 0; j < QPSK_FB; j++) {
                 const int s = s0 + j;
 #pragma unroll
                 for (int m = 0; m < 3; m++) {
@@ -589,22 +593,27 @@ struct DataJob {
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
+// one job float (compile-time index i < 112) from its source
+__device__ __forceinline__ float job_word(int i, const DataJob& j, const float* xf) {
+    if (i < 70) return xf[i];
+    if (i < 80) return (i & 1) ? j.k.eq[(i - 70) >> 1].y : j.k.eq[(i - 70) >> 1].x;
+    if (i < 100) return (i & 1) ? j.k.u[(i - 80) >> 1].y : j.k.u[(i - 80) >> 1].x;
+    if (i < 105) return j.k.d[i - 100].x;
+    if (i == 105) return __uint_as_float((unsigned)(j.cf & 0xffffffffu));
+    if (i == 106) return __uint_as_float((unsigned)(j.cf >> 32));
+    if (i == 107) return __uint_as_float(j.ks);
+    return 0.0f;
+}
+
+// Streamed: each 16-B store right after the window loads it needs (the job
+// queue may alias the window as far as the compiler knows, so staging the
+// whole job first would hold all 112 floats in registers).
 __device__ __forceinline__ void put_job(float4* out, const DataJob& j, const f2* x35) {
-    float v[112];
+    const float* xf = reinterpret_cast<const float*>(x35);
 #pragma unroll
-    for (int t = 0; t < 35; t++) { v[2 * t] = x35[t].x; v[2 * t + 1] = x35[t].y; }
-#pragma unroll
-    for (int t = 0; t < 5; t++) { v[70 + 2 * t] = j.k.eq[t].x; v[71 + 2 * t] = j.k.eq[t].y; }
-#pragma unroll
-    for (int t = 0; t < 10; t++) { v[80 + 2 * t] = j.k.u[t].x; v[81 + 2 * t] = j.k.u[t].y; }
-#pragma unroll
-    for (int t = 0; t < 5; t++) v[100 + t] = j.k.d[t].x;
-    v[105] = __uint_as_float((unsigned)(j.cf & 0xffffffffu));
-    v[106] = __uint_as_float((unsigned)(j.cf >> 32));
-    v[107] = __uint_as_float(j.ks);
-    v[108] = v[109] = v[110] = v[111] = 0.0f;
-#pragma unroll
-    for (int q = 0; q < kJobF4; q++) out[q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+    for (int q = 0; q < kJobF4; q++)
+        out[q] = make_float4(job_word(4 * q, j, xf), job_word(4 * q + 1, j, xf),
+                             job_word(4 * q + 2, j, xf), job_word(4 * q + 3, j, xf));
 }
 
 __device__ __forceinline__ void get_job(const float4* in, DataJob& j) {
@@ -829,10 +838,9 @@ __global__ void __launch_bounds__(64 * G * ((DUAL ? 2 : 1) + FP), 3) rx_kernel(
     float2* win0, float2* win1, int* mi0, int* mi1, int* rt0, int* rt1, uint8_t* bits,
     uint8_t* valid, int32_t* trace, float2* soft, float4* jobs, unsigned* njobs, int nch, int F,
     unsigned g0, int roles) {
-    static_assert(!DUAL || G == 1, "dual-chain backs: one group per workgroup");
-    static_assert(W == QK_GROUP || (DUAL && W % FP == 0 && W <= QK_GROUP), "group width");
+    static_assert(W == QK_GROUP || (DUAL && G == 1 && W % FP == 0 && W <= QK_GROUP), "group width");
     constexpr int kGroups = G, kFrontPer = FP;
-    constexpr int kBackWaves = DUAL ? 2 : kGroups;
+    constexpr int kBackWaves = DUAL ? 2 * kGroups : kGroups;
     constexpr int kFrontCh = W / kFrontPer;            // channels per front wave
     constexpr int kFrontWaves = kGroups * kFrontPer;
     constexpr int kBlock = 64 * (kBackWaves + kFrontWaves);
@@ -844,7 +852,7 @@ __global__ void __launch_bounds__(64 * G * ((DUAL ? 2 : 1) + FP), 3) rx_kernel(
     __shared__ __attribute__((aligned(16))) float2 decs[kFrontWaves][kDecBuf][kDec];
     __shared__ int mi_s[kGroups][2][QK_GROUP], rt_s[kGroups][2][QK_GROUP];
     __shared__ __attribute__((aligned(16))) float BT[qhunt::kBT];   // correlator's B
-    __shared__ int bseq[2], fcnt[2];   // DUAL progress counters
+    __shared__ int bseq[kGroups][2], fcnt[kGroups][2];   // DUAL progress counters, per group
     const int lane = threadIdx.x & 63;
     // wave-uniform by construction; readfirstlane tells the compiler, so every
     // per-wave index and pointer below lives in SGPRs
@@ -860,32 +868,35 @@ __global__ void __launch_bounds__(64 * G * ((DUAL ? 2 : 1) + FP), 3) rx_kernel(
             rt_s[wave][0][lane] = rt_of(a, a.g0)[ch];
         }
     }
-    if (threadIdx.x < 2) bseq[threadIdx.x] = fcnt[threadIdx.x] = 0;
+    if (threadIdx.x < 2 * kGroups) (&bseq[0][0])[threadIdx.x] = (&fcnt[0][0])[threadIdx.x] = 0;
     __syncthreads();
     if constexpr (DUAL) {
         if (wave < kBackWaves) {
-            // ---------------------------------------------------- back, frames n = wave mod 2
-            const int ch = grp0 * W + lane;
+            // ---------------------------------------------------- back of group wave/2,
+            // frames n = wave mod 2
+            const int gi = wave >> 1;
+            const int ch = (grp0 + gi) * W + lane;
             const bool live = lane < W && ch < a.nch;
             if (((a.roles >> 4) & 3) == 2) __builtin_amdgcn_s_setprio(2);
-            for (int n = wave; n < a.F; n += 2) {
+            for (int n = wave & 1; n < a.F; n += 2) {
                 const int p = n & 1;
-                // front(n-1) done by every front wave: window n and mi_n are in place
-                if (n > 0) spin_wait(&fcnt[p ^ 1], kFrontWaves * ((n - 1) / 2 + 1));
-                back_frame(a, live ? ch : 0, live, n, mi_s[0][p][lane],
+                // front(n-1) done by every front wave of the group: window n and mi_n
+                if (n > 0) spin_wait(&fcnt[gi][p ^ 1], kFrontPer * ((n - 1) / 2 + 1));
+                back_frame(a, live ? ch : 0, live, n, mi_s[gi][p][lane],
                            [&] {   // rx_timing of frame n = the decision of frame n-1
-                               if (n > 0) spin_wait(&bseq[p ^ 1], n);
-                               return rt_s[0][p][lane];
+                               if (n > 0) spin_wait(&bseq[gi][p ^ 1], n);
+                               return rt_s[gi][p][lane];
                            },
                            win_of(a, a.g0 + (unsigned)n) + (size_t)(live ? ch : 0) * kWinStride,
-                           &rt_s[0][p ^ 1][lane]);
-                signal_set(&bseq[p], n + 1, lane);
+                           &rt_s[gi][p ^ 1][lane]);
+                signal_set(&bseq[gi][p], n + 1, lane);
             }
         } else {
             // ---------------------------------------------------- front
             const int f = wave - kBackWaves;
-            const int cbeg = f * kFrontCh;
-            const int ch0 = grp0 * W + cbeg;
+            const int gi = f / kFrontPer;
+            const int cbeg = (f % kFrontPer) * kFrontCh;
+            const int ch0 = (grp0 + gi) * W + cbeg;
             const int nlive = max(0, min(kFrontCh, a.nch - ch0));
             float2* M = Ms[f];
             int pf[kPf<MODE>];
@@ -897,7 +908,7 @@ __global__ void __launch_bounds__(64 * G * ((DUAL ? 2 : 1) + FP), 3) rx_kernel(
                 float2* wout = win_of(a, g + 1u);
                 // back(n-1) done: rx_timing of frame n, and window n+1's buffer
                 // (window n-1) and mi_s[p ^ 1] (mi_{n-1}) are free
-                if (n > 0) spin_wait(&bseq[p ^ 1], n);
+                if (n > 0) spin_wait(&bseq[gi][p ^ 1], n);
                 int pmi = 0;
                 for (int c = 0; c < nlive; c++) {
                     const int ch = ch0 + c;
@@ -910,22 +921,23 @@ __global__ void __launch_bounds__(64 * G * ((DUAL ? 2 : 1) + FP), 3) rx_kernel(
                             prefetch<MODE>(srcs(a, same ? ch + 1 : ch0, same ? n : n + 1), lane, pf);
                     }
                     wave_lds_sync();
-                    pmi = front_channel<MODE>(lane, rt_s[0][p][cbeg + c], M, dcur, BT);
-                    if (lane == 0) mi_s[0][p ^ 1][cbeg + c] = pmi;
+                    pmi = front_channel<MODE>(lane, rt_s[gi][p][cbeg + c], M, dcur, BT);
+                    if (lane == 0) mi_s[gi][p ^ 1][cbeg + c] = pmi;
                     if (c + 1 == nlive) store_window(lane, pmi, dcur, wout + (size_t)ch * kWinStride);
                     wave_lds_sync();
                 }
-                signal_add(&fcnt[p], 1, lane);
+                signal_add(&fcnt[gi][p], 1, lane);
             }
             carry_history<MODE>(a.in, a.hist, a.F, ch0, nlive, lane);
         }
         __syncthreads();
-        if (wave == 0) {   // per-channel state after the call's last frame
-            const int ch = grp0 * W + lane;
+        if (wave < kBackWaves && (wave & 1) == 0) {   // state after the call's last frame
+            const int gi = wave >> 1;
+            const int ch = (grp0 + gi) * W + lane;
             if (lane < W && ch < a.nch) {
                 const unsigned ge = a.g0 + (unsigned)a.F;
-                mi_of(a, ge)[ch] = mi_s[0][a.F & 1][lane];
-                rt_of(a, ge)[ch] = rt_s[0][a.F & 1][lane];
+                mi_of(a, ge)[ch] = mi_s[gi][a.F & 1][lane];
+                rt_of(a, ge)[ch] = rt_s[gi][a.F & 1][lane];
             }
         }
         return;
@@ -1050,6 +1062,9 @@ struct qpsk_ctx {
     int shape_groups = 0;       // 0: by batch size; QPSK_SHAPE (A/B experiments)
     bool single_back = false;   // QPSK_SHAPE=1x8s: G = 1 without the dual-chain back
     int width = 0;              // dual-chain group width; 0: by batch size; QPSK_WIDTH
+    bool dual_multi = false;    // QPSK_SHAPE=4x1d: dual-chain backs, 4 groups x 1 front (A/B);
+                                // a 4x2 dual shape would need <= 128 VGPRs and spills
+    bool single2 = false;       // QPSK_SHAPE=2x4: 2 groups without the dual-chain backs
     float pend_ms[2] = {0.0f, 0.0f};
     int pend_frames = 0;
 };
@@ -1187,7 +1202,10 @@ extern "C" qpsk_ctx* qpsk_rx_create_mode(int device, int nch, int mode, int* err
     if (const char* sh = getenv("QPSK_SHAPE"))
     {
         c->shape_groups = !strcmp(sh, "1x8") || !strcmp(sh, "1x8s") ? 1
-                        : !strcmp(sh, "2x4") ? 2 : !strcmp(sh, "4x2") ? 4 : 0;
+                        : !strcmp(sh, "2x4") || !strcmp(sh, "2x4d") ? 2
+                        : !strcmp(sh, "4x2") || !strcmp(sh, "4x1d") ? 4 : 0;
+        c->dual_multi = !strcmp(sh, "4x1d");
+        c->single2 = !strcmp(sh, "2x4");
         c->single_back = !strcmp(sh, "1x8s");
     }
     int r = herr(hipSetDevice(device));
@@ -1285,6 +1303,9 @@ extern "C" int qpsk_rx_batch_device(qpsk_ctx* c, const int16_t* d_in, int F, uin
     // and the narrowest group width (64/32/16 channels) that still fits the
     // batch in one wave of workgroups (QPSK_WIDTH overrides)
     const bool dual = G == 1 && !c->single_back;
+    // two groups per workgroup: dual-chain backs too (2x4d; 11% faster at
+    // 32,768 channels, profiles/r01_dual_ab.txt) unless QPSK_SHAPE=2x4
+    const bool dual_multi = (c->dual_multi && G == 4) || (G == 2 && !c->single2);
     int W = 64;
     if (dual) {
         W = c->width > 0 ? c->width
@@ -1292,7 +1313,9 @@ extern "C" int qpsk_rx_batch_device(qpsk_ctx* c, const int16_t* d_in, int F, uin
     }
 #define QPSK_LAUNCH_MODE(MM)                                                                   \
     do {                                                                                       \
-        if (dual && W == 16) QPSK_LAUNCH(1, 8, MM, true, 16);                                  \
+        if (dual_multi && G == 4) QPSK_LAUNCH(4, 1, MM, true, 64);                             \
+        else if (dual_multi) QPSK_LAUNCH(2, 4, MM, true, 64);                                  \
+        else if (dual && W == 16) QPSK_LAUNCH(1, 8, MM, true, 16);                             \
         else if (dual && W == 32) QPSK_LAUNCH(1, 8, MM, true, 32);                             \
         else if (dual) QPSK_LAUNCH(1, 8, MM, true, 64);                                        \
         else if (G == 1) QPSK_LAUNCH(1, 8, MM, false, 64);                                     \
