@@ -921,7 +921,10 @@ __global__ void __launch_bounds__(64 * G * ((DUAL ? 2 : 1) + FP), 3) rx_kernel(
                             prefetch<MODE>(srcs(a, same ? ch + 1 : ch0, same ? n : n + 1), lane, pf);
                     }
                     wave_lds_sync();
-                    pmi = front_channel<MODE>(lane, rt_s[gi][p][cbeg + c], M, dcur, BT);
+#ifdef QPSK_STAMPS
+                    unsigned long long st_acc[16];   // dual-chain shapes are not stamped
+#endif
+                    pmi = front_channel<MODE>(lane, rt_s[gi][p][cbeg + c], M, dcur, BT FACC_ARG);
                     if (lane == 0) mi_s[gi][p ^ 1][cbeg + c] = pmi;
                     if (c + 1 == nlive) store_window(lane, pmi, dcur, wout + (size_t)ch * kWinStride);
                     wave_lds_sync();
