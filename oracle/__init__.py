@@ -64,6 +64,8 @@ def cpu_lib():
         lib.qc_synth_batch.argtypes = [C.c_uint64, C.c_uint32, C.c_int, C.c_double,
                                        C.c_void_p, C.c_long, C.c_int]
         lib.qc_mixer_table.argtypes = [C.c_void_p]
+        lib.qc_fft.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+        lib.qc_fft_twiddles.argtypes = [C.c_int, C.c_int, C.c_void_p]
         lib.qc_keystream.argtypes = [C.c_void_p, C.c_int]
         _cpu = lib
     return _cpu
@@ -223,3 +225,43 @@ def preamble() -> np.ndarray:
     vals = [int(v) for v in re.findall(r"-?\d+", body)]
     assert len(vals) == 128 and set(vals) == {-1, 1}
     return np.asarray(vals, np.int8)
+
+
+# ------------------------------------------------------------------- kiss_fft
+def cpu_fft(x, inverse: bool = False) -> np.ndarray:
+    """Restatement of the reference's fft() (src/fft.c) on a complex64 vector
+    (or [batch][nfft])."""
+    x = np.ascontiguousarray(x, dtype=np.complex64)
+    out = np.empty_like(x)
+    flat, fo = x.reshape(-1, x.shape[-1]), out.reshape(-1, x.shape[-1])
+    for b in range(flat.shape[0]):
+        r = cpu_lib().qc_fft(flat.shape[1], int(inverse), _p(flat[b]), _p(fo[b]))
+        assert r == 0
+    return out
+
+
+def fft_twiddles(nfft: int, inverse: bool = False) -> np.ndarray:
+    tw = np.empty(nfft, np.complex64)
+    cpu_lib().qc_fft_twiddles(nfft, int(inverse), _p(tw))
+    return tw
+
+
+def ref_fft_available() -> bool:
+    return os.path.exists(os.path.join(HERE, "_ref", "libkissfft_ref.so"))
+
+
+_kfr = None
+
+
+def ref_fft(x, inverse: bool = False) -> np.ndarray:
+    """The reference's own kiss_fft (oracle/_ref/libkissfft_ref.so)."""
+    global _kfr
+    if _kfr is None:
+        _kfr = C.CDLL(os.path.join(HERE, "_ref", "libkissfft_ref.so"))
+        _kfr.ref_fft.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+    x = np.ascontiguousarray(x, dtype=np.complex64)
+    out = np.empty_like(x)
+    flat, fo = x.reshape(-1, x.shape[-1]), out.reshape(-1, x.shape[-1])
+    for b in range(flat.shape[0]):
+        assert _kfr.ref_fft(flat.shape[1], int(inverse), _p(flat[b]), _p(fo[b])) == 0
+    return out

@@ -412,6 +412,183 @@ long qc_rx_batch_mode(const int16_t *in, int nch, int nframes, uint8_t *bits,
     return total;
 }
 
+/* ------------------------------------------------------------------ FFT */
+/* Restatement of the reference's kiss_fft (src/fft.c, Borgerding's kiss_fft
+ * as modified by the reference author).  Complex values are (re, im) float
+ * pairs; every operation below is the one gcc -O2 emits for the reference's
+ * C99 complex expressions with finite operands: a complex product is
+ * (ac - bd, ad + bc), complex * real is componentwise, and `x + y * I` is
+ * (x + y * 0.0f, y), `x - y * I` is (x - y * 0.0f, -y) (the y * 0.0f only
+ * decides the sign of a zero real part; checked on gcc 11.4's output).  Pinned bit for bit against the compiled reference
+ * (oracle/_ref/libkissfft_ref.so) by tests/test_oracle.py. */
+
+typedef struct { float r, i; } qc_cf;
+
+static inline qc_cf cf_mul(qc_cf a, qc_cf b) {
+    qc_cf o = {a.r * b.r - a.i * b.i, a.r * b.i + a.i * b.r};
+    return o;
+}
+static inline qc_cf cf_add(qc_cf a, qc_cf b) { qc_cf o = {a.r + b.r, a.i + b.i}; return o; }
+static inline qc_cf cf_sub(qc_cf a, qc_cf b) { qc_cf o = {a.r - b.r, a.i - b.i}; return o; }
+static inline qc_cf cf_mk(float x, float y) { qc_cf o = {x + y * 0.0f, y}; return o; }     /* x + y*I */
+static inline qc_cf cf_mkm(float x, float y) { qc_cf o = {x - y * 0.0f, -y}; return o; }   /* x - y*I */
+
+typedef struct {
+    int nfft, inverse;
+    int factors[64];
+    qc_cf *tw;
+} qc_fft_t;
+
+void qc_fft_twiddles(int nfft, int inverse, float *tw) {   /* src/fft.c:67-74 */
+    /* TAU (headers/qpsk_internal.h:60) is 2.0f * M_PI, and M_PI is math.h's
+     * double constant (the header's float fallback is #ifndef'd away), so the
+     * phase is evaluated in double and rounded once to the float variable. */
+    const double tau = 2.0f * 3.14159265358979323846;
+    for (int i = 0; i < nfft; i++) {
+        float phase = (float)(-tau * (float)i / (float)nfft);
+        if (inverse) phase *= -1.0f;
+        tw[2 * i] = cosf(phase);                             /* cmplx() :67 */
+        tw[2 * i + 1] = sinf(phase);
+    }
+}
+
+static void qc_kf_factor(int n, int *fac) {                  /* src/fft.c:433-459 */
+    int p = 4;
+    const float floor_sqrt = floorf(sqrtf((float)n));
+    do {
+        while (n % p) {
+            p = p == 4 ? 2 : p == 2 ? 3 : p + 2;
+            if (p > floor_sqrt) p = n;
+        }
+        n /= p;
+        *fac++ = p;
+        *fac++ = n;
+    } while (n > 1);
+}
+
+static void qc_bfly2(qc_cf *F, size_t fs, const qc_fft_t *st, int m) {   /* :190-211 */
+    const qc_cf *tw = st->tw;
+    for (int k = 0; k < m; k++, tw += fs) {
+        const qc_cf t = cf_mul(F[m + k], *tw);
+        F[m + k] = cf_sub(F[k], t);
+        F[k] = cf_add(F[k], t);
+    }
+}
+
+static void qc_bfly4(qc_cf *F, size_t fs, const qc_fft_t *st, size_t m) {   /* :213-255 */
+    for (size_t k = 0; k < m; k++) {
+        qc_cf *f = F + k;
+        const qc_cf s0 = cf_mul(f[m], st->tw[k * fs]);
+        const qc_cf s1 = cf_mul(f[2 * m], st->tw[2 * k * fs]);
+        const qc_cf s2 = cf_mul(f[3 * m], st->tw[3 * k * fs]);
+        const qc_cf s5 = cf_sub(f[0], s1);
+        f[0] = cf_add(f[0], s1);
+        const qc_cf s3 = cf_add(s0, s2);
+        const qc_cf s4 = cf_sub(s0, s2);
+        f[2 * m] = cf_sub(f[0], s3);
+        f[0] = cf_add(f[0], s3);
+        if (st->inverse) {
+            f[m] = cf_mk(s5.r - s4.i, s5.i + s4.r);
+            f[3 * m] = cf_mk(s5.r + s4.i, s5.i - s4.r);
+        } else {
+            f[m] = cf_mk(s5.r + s4.i, s5.i - s4.r);
+            f[3 * m] = cf_mk(s5.r - s4.i, s5.i + s4.r);
+        }
+    }
+}
+
+static void qc_bfly3(qc_cf *F, size_t fs, const qc_fft_t *st, size_t m) {   /* :257-290 */
+    const qc_cf epi3 = st->tw[fs * m];
+    for (size_t k = 0; k < m; k++) {
+        qc_cf *f = F + k;
+        const qc_cf s1 = cf_mul(f[m], st->tw[k * fs]);
+        const qc_cf s2 = cf_mul(f[2 * m], st->tw[2 * k * fs]);
+        const qc_cf s3 = cf_add(s1, s2);
+        qc_cf s0 = cf_sub(s1, s2);
+        f[m] = cf_mk(f[0].r - s3.r * .5f, f[0].i - s3.i * .5f);
+        s0 = (qc_cf){s0.r * epi3.i, s0.i * epi3.i};
+        f[0] = cf_add(f[0], s3);
+        f[2 * m] = cf_mk(f[m].r + s0.i, f[m].i - s0.r);
+        f[m] = cf_mk(f[m].r - s0.i, f[m].i + s0.r);
+    }
+}
+
+static void qc_bfly5(qc_cf *F, size_t fs, const qc_fft_t *st, int m) {   /* :292-344 */
+    const qc_cf ya = st->tw[fs * m], yb = st->tw[fs * m * 2];
+    for (int u = 0; u < m; u++) {
+        qc_cf *f0 = F + u, *f1 = f0 + m, *f2 = f0 + 2 * m, *f3 = f0 + 3 * m, *f4 = f0 + 4 * m;
+        const qc_cf s0 = *f0;
+        const qc_cf s1 = cf_mul(*f1, st->tw[fs * u]);
+        const qc_cf s2 = cf_mul(*f2, st->tw[fs * 2 * u]);
+        const qc_cf s3 = cf_mul(*f3, st->tw[fs * 3 * u]);
+        const qc_cf s4 = cf_mul(*f4, st->tw[fs * 4 * u]);
+        const qc_cf s7 = cf_add(s1, s4), s10 = cf_sub(s1, s4);
+        const qc_cf s8 = cf_add(s2, s3), s9 = cf_sub(s2, s3);
+        *f0 = cf_add(*f0, cf_mk(s7.r + s8.r, s7.i + s8.i));
+        const qc_cf s5 = cf_mk((s0.r + s7.r * ya.r) + s8.r * yb.r, (s0.i + s7.i * ya.r) + s8.i * yb.r);
+        const qc_cf s6 = cf_mkm(-(s10.i * ya.i + s9.i * yb.i), s10.r * ya.i - s9.r * yb.i);
+        *f1 = cf_sub(s5, s6);
+        *f4 = cf_add(s5, s6);
+        const qc_cf s11 = cf_mk((s0.r + s7.r * yb.r) + s8.r * ya.r, (s0.i + s7.i * yb.r) + s8.i * ya.r);
+        /* as written at :327 (upstream kiss_fft has -a + b here, not -(a + b)) */
+        const qc_cf s12 = cf_mk(-(s10.i * yb.i + s9.i * ya.i), s10.r * yb.i - s9.r * ya.i);
+        *f2 = cf_add(s11, s12);
+        *f3 = cf_sub(s11, s12);
+    }
+}
+
+static void qc_bfly_generic(qc_cf *F, size_t fs, const qc_fft_t *st, int m, int p) {   /* :346-386 */
+    qc_cf *scratch = (qc_cf *)malloc(sizeof(qc_cf) * (size_t)p);
+    for (int u = 0; u < m; u++) {
+        int k = u;
+        for (int q1 = 0; q1 < p; q1++, k += m) scratch[q1] = F[k];
+        k = u;
+        for (int q1 = 0; q1 < p; q1++, k += m) {
+            int twidx = 0;
+            F[k] = scratch[0];
+            for (int q = 1; q < p; q++) {
+                twidx += (int)fs * k;
+                if (twidx >= st->nfft) twidx -= st->nfft;
+                F[k] = cf_add(F[k], cf_mul(scratch[q], st->tw[twidx]));
+            }
+        }
+    }
+    free(scratch);
+}
+
+static void qc_kf_work(qc_cf *Fout, const qc_cf *f, size_t fs, const int *fac,
+                       const qc_fft_t *st) {                 /* :388-431 */
+    const int p = fac[0], m = fac[1];
+    if (m == 1) {
+        for (int j = 0; j < p; j++) Fout[j] = f[(size_t)j * fs];
+    } else {
+        for (int j = 0; j < p; j++) qc_kf_work(Fout + (size_t)j * m, f + (size_t)j * fs, fs * p, fac + 2, st);
+    }
+    switch (p) {
+        case 2: qc_bfly2(Fout, fs, st, m); break;
+        case 3: qc_bfly3(Fout, fs, st, (size_t)m); break;
+        case 4: qc_bfly4(Fout, fs, st, (size_t)m); break;
+        case 5: qc_bfly5(Fout, fs, st, m); break;
+        default: qc_bfly_generic(Fout, fs, st, m, p);
+    }
+}
+
+int qc_fft(int nfft, int inverse, const float *in, float *out) {
+    if (nfft < 1) return -1;
+    qc_fft_t st;
+    st.nfft = nfft;
+    st.inverse = inverse;
+    st.tw = (qc_cf *)malloc(sizeof(qc_cf) * (size_t)nfft);
+    qc_fft_twiddles(nfft, inverse, (float *)st.tw);
+    qc_kf_factor(nfft, st.factors);
+    qc_cf *tmp = (qc_cf *)malloc(sizeof(qc_cf) * (size_t)nfft);   /* fft_stride(): in may == out */
+    qc_kf_work(tmp, (const qc_cf *)in, 1, st.factors, &st);
+    memcpy(out, tmp, sizeof(qc_cf) * (size_t)nfft);
+    free(tmp);
+    free(st.tw);
+    return 0;
+}
+
 /* ------------------------------------------------------------------ TX */
 
 void qc_tx_init(qc_tx_t *tx) {

@@ -76,6 +76,14 @@ void qc_mixer_table(float p[QC_FRAME][2]);
 /* RX descrambler keystream bits ks[0..n) (src/scramble.c:57-69, seed 0x4A80). */
 void qc_keystream(uint8_t *ks, int n);
 
+/* ---- kiss_fft restatement (src/fft.c; no caller in the reference) ------- */
+/* fft_alloc(nfft, inverse) + fft() (headers/fft.h:45-46) on nfft interleaved
+ * (re, im) pairs; any nfft >= 1 (radix 4, 2, 3, 5 and generic stages).
+ * Returns 0, or -1 for nfft < 1. */
+int qc_fft(int nfft, int inverse, const float *in, float *out);
+/* the twiddle table fft_alloc() builds (src/fft.c:67-74), nfft pairs */
+void qc_fft_twiddles(int nfft, int inverse, float *tw);
+
 /* ---- transmitter restatement (src/qpsk.c:251-342) ---------------------- */
 typedef struct {
     float fir_mem[QC_NTAPS][2];  /* tx_filter, src/qpsk.c:39   */

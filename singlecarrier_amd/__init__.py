@@ -100,6 +100,14 @@ def lib():
         L.qpsk_stream_ctx.argtypes = [vp]
         L.qpsk_records.restype = C.c_size_t
         L.qpsk_records.argtypes = [vp, vp, i32, vp]
+        L.qpsk_fft_alloc.restype = vp
+        L.qpsk_fft_alloc.argtypes = [i32, i32, i32, C.POINTER(C.c_int)]
+        L.qpsk_fft_free.argtypes = [vp]
+        L.qpsk_fft_device.argtypes = [vp, vp, vp, i32, vp]
+        L.qpsk_fft.argtypes = [vp, vp, vp, i32]
+        L.qpsk_fft_twiddle_table.restype = None
+        L.qpsk_fft_twiddle_table.argtypes = [i32, i32, vp]
+        L.qpsk_fft_perm_table.argtypes = [i32, vp]
         L.cnormf.restype = C.c_float
         L.cnormf.argtypes = [_CF]   # _Complex float == {float, float} in one SSE reg (SysV)
         _lib = L
@@ -114,7 +122,8 @@ SYMBOLS = ["qpsk_rx_create", "qpsk_rx_create_mode", "qpsk_rx_mode", "qpsk_rx_des
            "qpsk_rx_timing_collect", "qpsk_rx_timing_split", "qpsk_synth_device",
            "qpsk_tx_phase_table", "qpsk_stream_create", "qpsk_stream_destroy",
            "qpsk_stream_acquire", "qpsk_stream_submit", "qpsk_stream_pending",
-           "qpsk_stream_retrieve", "qpsk_stream_ctx", "qpsk_records"]
+           "qpsk_stream_retrieve", "qpsk_stream_ctx", "qpsk_records", "qpsk_fft_alloc",
+           "qpsk_fft_free", "qpsk_fft_device", "qpsk_fft"]
 
 
 def _check(rc: int) -> None:
@@ -368,3 +377,49 @@ def records(bits: np.ndarray, valid: np.ndarray) -> bytes:
     out = np.empty(max(nf, 1) * BITS_PER_FRAME, np.uint8)
     n = lib().qpsk_records(_ptr(bits), _ptr(valid), nf, _ptr(out))
     return out[:n].tobytes()
+
+
+class FftPlan:
+    """The reference's kiss_fft on the GPU (include/qpsk_fft.h): fft_alloc(nfft,
+    inverse) + batched fft(), bit-identical to src/fft.c.  nfft: a power of two
+    in [4, 4096]."""
+
+    def __init__(self, nfft: int, inverse: bool = False, device: int = 0):
+        err = C.c_int(0)
+        self._h = lib().qpsk_fft_alloc(device, nfft, int(inverse), C.byref(err))
+        if not self._h:
+            _check(err.value or -3)
+        self.nfft, self.inverse, self.device = nfft, bool(inverse), device
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            lib().qpsk_fft_free(self._h)
+            self._h = None
+
+    __del__ = close
+
+    def __call__(self, x) -> np.ndarray:
+        """complex64 [..., nfft] host array -> its transform (host)."""
+        x = np.ascontiguousarray(x, dtype=np.complex64)
+        if x.shape[-1] != self.nfft:
+            raise ValueError(f"last axis must be {self.nfft}")
+        out = np.empty_like(x)
+        _check(lib().qpsk_fft(self._h, _ptr(x), _ptr(out), x.size // self.nfft))
+        return out
+
+    def run_device(self, x, out=None, stream=None):
+        """torch complex64 (or float32 [..., nfft, 2]) cuda tensors; enqueued."""
+        import torch
+        if out is None:
+            out = torch.empty_like(x)
+        n = x.numel() // (self.nfft * (1 if x.is_complex() else 2))
+        s = stream if stream is not None else torch.cuda.current_stream(x.device)
+        _check(lib().qpsk_fft_device(self._h, x.data_ptr(), out.data_ptr(), n, s.cuda_stream))
+        return out
+
+
+def fft_twiddle_table(nfft: int, inverse: bool = False) -> np.ndarray:
+    """The product's host twiddle table (qpsk_fft_host.c), for tests."""
+    tw = np.empty(nfft, np.complex64)
+    lib().qpsk_fft_twiddle_table(nfft, int(inverse), _ptr(tw))
+    return tw

@@ -127,3 +127,22 @@ def test_create_mode_rejects_unknown_modes():
         assert not L.qpsk_rx_create_mode(0, nch, mode, C.byref(err))
         assert err.value == -1   # QPSK_EINVAL
     assert L.qpsk_rx_mode(None) == -1
+
+
+def test_fft_host_twiddles_match_the_reference_formula():
+    """The product's twiddle table (qpsk_fft_host.c) has the bits of the
+    reference's fft_alloc (src/fft.c:67-74), via the oracle restatement (itself
+    pinned to the compiled reference in tests/test_oracle.py)."""
+    import oracle
+    for n in (4, 8, 64, 256, 512, 4096):
+        for inv in (False, True):
+            np.testing.assert_array_equal(sc.fft_twiddle_table(n, inv).view(np.uint32),
+                                          oracle.fft_twiddles(n, inv).view(np.uint32))
+
+
+def test_fft_alloc_rejects_unsupported_sizes():
+    import ctypes as C
+    for n in (0, 2, 3, 12, 100, 8192):
+        err = C.c_int(0)
+        assert not sc.lib().qpsk_fft_alloc(0, n, 0, C.byref(err))
+        assert err.value == -1

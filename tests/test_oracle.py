@@ -181,3 +181,37 @@ def test_dec752_random_channels_vs_padded_reference(ebn0):
         np.testing.assert_array_equal(t1[k], t2[k])
     vm = v2.astype(bool)
     np.testing.assert_array_equal(t1["soft"][vm], t2["soft"][vm])
+
+
+# ---------------------------------------------------------------- kiss_fft
+# The reference's FFT (src/fft.c; nothing in the reference calls it) restated in
+# oracle/cpu_ref.c (qc_fft), diffed bit for bit against the compiled reference:
+# every radix (4, 2, 3, 5, generic), forward and inverse, signed zeros.
+FFT_SIZES = [1, 2, 3, 4, 5, 6, 7, 8, 12, 15, 16, 25, 60, 64, 100, 128, 243, 256, 343, 512,
+             1000, 1024, 4096]
+
+
+@pytest.mark.parametrize("n", FFT_SIZES)
+def test_fft_restatement_vs_reference(n):
+    if not oracle.ref_fft_available():
+        pytest.skip("oracle/_ref not built (no /root/reference here)")
+    rng = np.random.default_rng(n)
+    cases = [
+        (rng.standard_normal(n) + 1j * rng.standard_normal(n)),
+        rng.integers(-3, 4, n) + 1j * rng.integers(-3, 4, n),
+        rng.standard_normal(n) * 1e4,
+    ]
+    z = np.zeros(n, np.complex64)
+    z.view(np.float32)[:] = rng.choice([-0.0, 0.0, 1.0, -1.0], 2 * n)
+    cases.append(z)
+    for x in cases:
+        x = np.asarray(x, np.complex64)
+        for inv in (False, True):
+            np.testing.assert_array_equal(oracle.cpu_fft(x, inv).view(np.uint32),
+                                          oracle.ref_fft(x, inv).view(np.uint32))
+
+
+def test_fft_restatement_is_a_dft():
+    x = (np.random.default_rng(3).standard_normal(256) * (1 + 1j)).astype(np.complex64)
+    np.testing.assert_allclose(oracle.cpu_fft(x), np.fft.fft(x), atol=1e-4)
+    np.testing.assert_allclose(oracle.cpu_fft(x, True), np.fft.ifft(x) * 256, atol=1e-4)
