@@ -33,6 +33,11 @@ VALU_PEAK_TOPS = 78.6               # fp32 non-FMA lane-ops/s: 256 CU x 128 lane
 OPS_PER_SAMPLE_MIN = 96.0           # minimal bit-exact formulation
 
 
+# receiver semantics (include/qpsk_batch.h QPSK_MODE_*): reference parity, the
+# dec752 buffer, the kiss_fft hunt, both (not parity)
+MODES = {"reference": 0, "dec752": 1, "fft": 2, "dec752fft": 3}
+
+
 def shard(channels: int, world: int, rank: int, strong: bool):
     """(channels on this rank, first global channel id).  Weak: every rank
     demodulates its own `channels`-channel batch (distinct channel ids); strong:
@@ -66,9 +71,10 @@ def parse():
     ap.add_argument("--ebn0", type=float, default=1000.0, help=">= 100: noiseless")
     ap.add_argument("--seed", type=int, default=3)
     ap.add_argument("--strong", action="store_true", help="split --channels across ranks")
-    ap.add_argument("--mode", choices=("reference", "dec752"), default="reference",
-                    help="receiver semantics: reference parity (default) or dec752 "
-                         "(decimated_frame[752], SURVEY.md 8f rank 3; not reference parity)")
+    ap.add_argument("--mode", choices=tuple(MODES), default="reference",
+                    help="receiver semantics: reference parity (default); dec752 "
+                         "(decimated_frame[752]), fft (kiss_fft hunt) or both: SURVEY.md 8f "
+                         "rank 3 variants, not reference parity")
     ap.add_argument("--cpu-channels", type=int, default=4096,
                     help="channels of the bounded CPU-baseline sample (0: skip)")
     ap.add_argument("--verify", type=int, default=256,
@@ -229,7 +235,7 @@ def main():
     if rank0 and world == 1 and args.cpu_all_channels > 0 and args.cpu_procs > 1:
         import multiprocessing as mp
         import oracle
-        if oracle.ref_available(1 if args.mode == "dec752" else 0):
+        if oracle.ref_available(MODES[args.mode]):
             pool = mp.get_context("spawn").Pool(args.cpu_procs)   # before any GPU use
 
     import torch
@@ -264,7 +270,7 @@ def main():
         del x2
     bits = torch.empty((nch, nf, 62), dtype=torch.uint8, device=x.device)
     valid = torch.empty((nch, nf), dtype=torch.uint8, device=x.device)
-    mode = sc.MODE_DEC752 if args.mode == "dec752" else sc.MODE_REFERENCE
+    mode = MODES[args.mode]
     rx = sc.Receiver(nch, device=local, mode=mode)
 
     for _ in range(args.warmup):

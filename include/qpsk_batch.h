@@ -54,6 +54,13 @@ enum {
                                  variant, NOT reference parity; equal to the
                                  unmodified reference sources linked with that
                                  array padded (oracle/ref/dec752.ld) */
+    QPSK_MODE_FFT_HUNT = 2,   /* flag, combinable with either of the above: the
+                                 preamble hunt correlates through the reference's
+                                 kiss_fft (src/fft.c, which the reference never
+                                 calls): S = ifft(fft(dec[0..255]) * conj(fft(c))),
+                                 c = conj(preambletable) zero-padded to 256, then
+                                 the hunt loop of src/qpsk.c:172-183 over
+                                 cnormf(S[l]).  Not reference parity. */
 };
 
 /* Create a receiver for nch channels on HIP device `device`, in the reference's

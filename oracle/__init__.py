@@ -66,6 +66,9 @@ def cpu_lib():
         lib.qc_mixer_table.argtypes = [C.c_void_p]
         lib.qc_fft.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_void_p]
         lib.qc_fft_twiddles.argtypes = [C.c_int, C.c_int, C.c_void_p]
+        lib.qc_fft_hunt.restype = C.c_int
+        lib.qc_fft_hunt.argtypes = [C.c_void_p]
+        lib.qc_fft_hunt_spectrum.argtypes = [C.c_void_p]
         lib.qc_keystream.argtypes = [C.c_void_p, C.c_int]
         _cpu = lib
     return _cpu
@@ -74,11 +77,13 @@ def cpu_lib():
 # receiver semantics (cpu_ref.h QC_MODE_*; singlecarrier_amd.MODE_*)
 MODE_REF = 0      # the reference as built (gcc -O2, "model A" overflow)
 MODE_DEC752 = 1   # decimated_frame[752] ("intended semantics", NOT reference parity)
-_REF_LIBS = {MODE_REF: "libqpsk_ref.so", MODE_DEC752: "libqpsk_ref752.so"}
+MODE_FFT_HUNT = 2  # flag: the preamble hunt correlates through kiss_fft (src/fft.c)
+_REF_LIBS = {MODE_REF: "libqpsk_ref.so", MODE_DEC752: "libqpsk_ref752.so"}   # no FFT-hunt build:
+# the reference never calls its FFT; that variant is pinned per component
 
 
 def ref_available(mode: int = MODE_REF) -> bool:
-    return os.path.exists(os.path.join(HERE, "_ref", _REF_LIBS[mode]))
+    return mode in _REF_LIBS and os.path.exists(os.path.join(HERE, "_ref", _REF_LIBS[mode]))
 
 
 def ref_lib(mode: int = MODE_REF):
@@ -265,3 +270,15 @@ def ref_fft(x, inverse: bool = False) -> np.ndarray:
     for b in range(flat.shape[0]):
         assert _kfr.ref_fft(flat.shape[1], int(inverse), _p(flat[b]), _p(fo[b])) == 0
     return out
+
+
+def fft_hunt(dec) -> int:
+    """qc_fft_hunt: max_index of the FFT-correlation hunt over dec[0..255]."""
+    d = np.ascontiguousarray(np.asarray(dec, np.complex64)[:256])
+    return int(cpu_lib().qc_fft_hunt(_p(d)))
+
+
+def fft_hunt_spectrum() -> np.ndarray:
+    q = np.empty(256, np.complex64)
+    cpu_lib().qc_fft_hunt_spectrum(_p(q))
+    return q

@@ -268,7 +268,7 @@ int qc_rx_frame(qc_chan_t *ch, const int16_t in[QC_FRAME], uint8_t bits[QC_BITS]
                 qc_trace_t *tr) {
     const uint32_t n = ch->frame;
     const int rt = ch->rx_timing;
-    const int d752 = ch->mode == QC_MODE_DEC752;
+    const int d752 = (ch->mode & QC_MODE_DEC752) != 0;
     /* M[-48..hi]: m_{n-2}[1832..1879] ++ m_{n-1}[0..hi] (zero before frame 0);
      * hi = 1190 (model A, D_n[0..187]) or 1700 (dec752, D_n[0..289]) */
     enum { LO = QC_NTAPS - 1, HIMAX = 5 * (QC_DEC752 - 1) + 255 };
@@ -296,13 +296,16 @@ int qc_rx_frame(qc_chan_t *ch, const int16_t in[QC_FRAME], uint8_t bits[QC_BITS]
     }
 
     /* preamble hunt, src/qpsk.c:172-183 */
+    int mi = 0;
+    if (ch->mode & QC_MODE_FFT_HUNT) {
+        mi = qc_fft_hunt(&dec[0][0]);
+    } else {
     float T[255], U[255];
     for (int j = 0; j < 255; j++) {
         T[j] = dec[j][0] - dec[j][1];
         U[j] = dec[j][1] + dec[j][0];
     }
     float max_value = 0.0f;
-    int mi = 0;
     for (int L = 0; L < QC_PRE; L++) {
         float sr = 0.0f, si = 0.0f;
         for (int i = 0; i < QC_PRE; i++) {
@@ -319,6 +322,7 @@ int qc_rx_frame(qc_chan_t *ch, const int16_t in[QC_FRAME], uint8_t bits[QC_BITS]
             max_value = c;
             mi = L;
         }
+    }
     }
 
     /* equalize(), src/qpsk.c:111-123 */
@@ -587,6 +591,51 @@ int qc_fft(int nfft, int inverse, const float *in, float *out) {
     free(tmp);
     free(st.tw);
     return 0;
+}
+
+static float g_fftq[256][2];
+static pthread_once_t g_fftq_once = PTHREAD_ONCE_INIT;
+
+static void init_fftq(void) {
+    float c[256][2];
+    memset(c, 0, sizeof c);
+    for (int i = 0; i < QC_PRE; i++) {   /* conj(preambletable[i]) = (p, -p) */
+        c[i][0] = (float)k_pre[i];
+        c[i][1] = -(float)k_pre[i];
+    }
+    float C[256][2];
+    qc_fft(256, 0, &c[0][0], &C[0][0]);
+    for (int k = 0; k < 256; k++) {
+        g_fftq[k][0] = C[k][0];
+        g_fftq[k][1] = -C[k][1];
+    }
+}
+
+void qc_fft_hunt_spectrum(float *q) {
+    pthread_once(&g_fftq_once, init_fftq);
+    memcpy(q, g_fftq, sizeof g_fftq);
+}
+
+int qc_fft_hunt(const float *dec) {
+    pthread_once(&g_fftq_once, init_fftq);
+    float X[256][2], Y[256][2], S[256][2];
+    qc_fft(256, 0, dec, &X[0][0]);
+    for (int k = 0; k < 256; k++) {   /* complex product, (ac - bd, ad + bc) */
+        const qc_cf p = cf_mul((qc_cf){X[k][0], X[k][1]}, (qc_cf){g_fftq[k][0], g_fftq[k][1]});
+        Y[k][0] = p.r;
+        Y[k][1] = p.i;
+    }
+    qc_fft(256, 1, &Y[0][0], &S[0][0]);
+    float max_value = 0.0f;
+    int mi = 0;
+    for (int L = 0; L < QC_PRE; L++) {   /* src/qpsk.c:172-183 */
+        const float c = S[L][0] * S[L][0] + S[L][1] * S[L][1];   /* cnormf :75-80 */
+        if (c > max_value) {
+            max_value = c;
+            mi = L;
+        }
+    }
+    return mi;
 }
 
 /* ------------------------------------------------------------------ TX */

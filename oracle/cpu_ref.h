@@ -37,6 +37,8 @@ extern "C" {
                                 assumes (src/qpsk.c:157-162): NOT reference
                                 parity; pinned by the layout-padded reference
                                 build oracle/_ref/libqpsk_ref752.so           */
+#define QC_MODE_FFT_HUNT 2   /* flag: the preamble hunt correlates through the
+                                reference's kiss_fft (src/fft.c), see qc_fft_hunt */
 
 /* Explicit per-channel receiver state (the reference keeps it in statics,
  * src/qpsk.c:37-53, src/scramble.c:41-42). */
@@ -83,6 +85,15 @@ void qc_keystream(uint8_t *ks, int n);
 int qc_fft(int nfft, int inverse, const float *in, float *out);
 /* the twiddle table fft_alloc() builds (src/fft.c:67-74), nfft pairs */
 void qc_fft_twiddles(int nfft, int inverse, float *tw);
+/* The FFT-correlation hunt of the QC_MODE_FFT_HUNT receiver variant over
+ * dec[0..255] (interleaved pairs):  S = ifft(fft(dec) * Q) with
+ * Q = conj(fft(c)), c[i] = conj(preambletable[i]) = (p_i, -p_i) for i < 128
+ * and 0 above (256-point kiss_fft, unnormalized; S[l] = 256 x the correlate()
+ * sum of src/qpsk.c:88-96 in exact arithmetic); then the reference's hunt
+ * loop (src/qpsk.c:172-183) over cnormf(S[l]), l < 128.  Returns max_index. */
+int qc_fft_hunt(const float *dec);
+/* Q above (256 pairs), for tests */
+void qc_fft_hunt_spectrum(float *q);
 
 /* ---- transmitter restatement (src/qpsk.c:251-342) ---------------------- */
 typedef struct {

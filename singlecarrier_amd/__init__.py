@@ -142,6 +142,7 @@ def _ptr(a) -> int | None:
 # receiver semantics (include/qpsk_batch.h QPSK_MODE_*)
 MODE_REFERENCE = 0   # bit-identical to the reference as built
 MODE_DEC752 = 1      # decimated_frame[752] ("intended semantics"), NOT reference parity
+MODE_FFT_HUNT = 2    # flag: preamble hunt through the reference's kiss_fft (src/fft.c)
 
 
 class Receiver:

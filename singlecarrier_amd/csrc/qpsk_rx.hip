@@ -29,7 +29,10 @@
 #include <utility>
 
 #include "qpsk_batch.h"
+#include "qpsk_fft.h"
 #include "qpsk_consts.h"
+#include "qpsk_fft_dev.h"
+#include "qpsk_fft_tables.h"
 #include "qpsk_hunt.h"
 #include "qpsk_rcp.h"
 
@@ -324,13 +327,48 @@ __device__ __forceinline__ void fir_dec752(int lane, int rt, const float2* M, fl
     }
 }
 
+// The FFT-correlation hunt of the QPSK_MODE_FFT_HUNT variant (cpu_ref.h
+// qc_fft_hunt): S = ifft(fft(dec[0..255]) * Q) with the reference's kiss_fft
+// (qpsk_fft_dev.h, bit-identical to src/fft.c), then the hunt loop of
+// src/qpsk.c:172-183 over cnormf(S[l]), l < 128.  The two 256-point buffers
+// reuse M (free after the FIR).  HT (LDS): twiddles forward [0, 256) and
+// inverse [256, 512), Q [512, 768) as (re, im) pairs, then kf_work's input
+// permutation as 256 ints.
+constexpr int kFftHT = 768 * 2 + 256;   // floats
+__device__ __forceinline__ int fft_hunt(int lane, float2* M, const float2* dec, const float* HT) {
+    const qfft::cf* tw = reinterpret_cast<const qfft::cf*>(HT);
+    const int* perm = reinterpret_cast<const int*>(HT + 768 * 2);
+    qfft::cf* X = reinterpret_cast<qfft::cf*>(M);
+    qfft::cf* Y = X + 256;
+    const qfft::cf* d = reinterpret_cast<const qfft::cf*>(dec);
+    for (int pos = lane; pos < 256; pos += 64) X[pos] = d[perm[pos]];   // kf_work leaves
+    qfft::lds_sync();
+    qfft::stages(lane, 256, X, tw, false);
+    for (int pos = lane; pos < 256; pos += 64) {   // Y = X * Q, in the inverse's leaf order
+        const int k = perm[pos];
+        Y[pos] = qfft::mul(X[k], tw[512 + k]);
+    }
+    qfft::lds_sync();
+    qfft::stages(lane, 256, Y, tw + 256, true);
+    const qfft::cf s0 = Y[lane], s1 = Y[lane + 64];   // lags lane and 64 + lane
+    const float c0 = s0.r * s0.r + s0.i * s0.i;       // cnormf, src/qpsk.c:75-80
+    const float c1 = s1.r * s1.r + s1.i * s1.i;
+    const unsigned k0 = c0 > 0.0f ? __float_as_uint(c0) : 0u;   // as the direct hunt below
+    const unsigned k1 = c1 > 0.0f ? __float_as_uint(c1) : 0u;
+    const unsigned km = wave_max_u32(max(k0, k1));
+    qfft::lds_sync();   // X / Y (M) are rewritten by the next channel's mixer
+    if (km == 0u) return 0;
+    const unsigned long long m0 = __ballot(k0 == km), m1 = __ballot(k1 == km);
+    return m0 ? __ffsll((long long)m0) - 1 : 64 + __ffsll((long long)m1) - 1;
+}
+
 template <int MODE>
 __device__ __forceinline__ int front_channel(int lane, int rt, float2* M, float2* dec,
                                              const float* BT FACC_PARAM) {
 #ifdef QPSK_STAMPS
     unsigned long long ft0 = stamp_now();
 #endif
-    if constexpr (MODE == 1) {
+    if constexpr ((MODE & 1) != 0) {
         fir_dec752(lane, rt, M, dec);
         FSTAMP(0);
     } else {
@@ -392,6 +430,7 @@ __device__ __forceinline__ int front_channel(int lane, int rt, float2* M, float2
     }
     wave_lds_sync();
     FSTAMP(1);
+    if constexpr ((MODE & 2) != 0) return fft_hunt(lane, M, dec, BT);
     // correlate (src/qpsk.c:88-96) for all 128 lags on the matrix cores
     // (qpsk_hunt.h: bit-identical k-ordered chain); the TK image reuses M.
     float* TK = reinterpret_cast<float*>(M);
@@ -837,7 +876,7 @@ __global__ void __launch_bounds__(64 * G * ((DUAL ? 2 : 1) + FP), 3) rx_kernel(
     const int16_t* in, int16_t* hist, const float2* ptab, const unsigned long long* ks,
     float2* win0, float2* win1, int* mi0, int* mi1, int* rt0, int* rt1, uint8_t* bits,
     uint8_t* valid, int32_t* trace, float2* soft, float4* jobs, unsigned* njobs, int nch, int F,
-    unsigned g0, int roles) {
+    unsigned g0, int roles, const float* fft_tab) {
     static_assert(W == QK_GROUP || (DUAL && G == 1 && W % FP == 0 && W <= QK_GROUP), "group width");
     constexpr int kGroups = G, kFrontPer = FP;
     constexpr int kBackWaves = DUAL ? 2 * kGroups : kGroups;
@@ -847,11 +886,13 @@ __global__ void __launch_bounds__(64 * G * ((DUAL ? 2 : 1) + FP), 3) rx_kernel(
     const RxArgs a{in, hist, ptab, ks, win0, win1, mi0, mi1, rt0, rt1, bits, valid, trace, soft,
                    jobs, njobs, nch, F, g0, roles};
     __shared__ __attribute__((aligned(16))) float2 P[QK_FRAME];
-    constexpr int kM = Cfg<MODE>::kM, kDecBuf = Cfg<MODE>::kDecBuf;
+    constexpr int DM = MODE & 1;   // decimation semantics; MODE & 2: FFT hunt
+    constexpr int kM = Cfg<DM>::kM, kDecBuf = Cfg<DM>::kDecBuf;
     __shared__ __attribute__((aligned(16))) float2 Ms[kFrontWaves][kM];
     __shared__ __attribute__((aligned(16))) float2 decs[kFrontWaves][kDecBuf][kDec];
     __shared__ int mi_s[kGroups][2][QK_GROUP], rt_s[kGroups][2][QK_GROUP];
-    __shared__ __attribute__((aligned(16))) float BT[qhunt::kBT];   // correlator's B
+    // hunt tables: the MFMA correlator's B, or the FFT hunt's twiddles / Q / permutation
+    __shared__ __attribute__((aligned(16))) float BT[(MODE & 2) ? kFftHT : qhunt::kBT];
     __shared__ int bseq[kGroups][2], fcnt[kGroups][2];   // DUAL progress counters, per group
     const int lane = threadIdx.x & 63;
     // wave-uniform by construction; readfirstlane tells the compiler, so every
@@ -860,7 +901,11 @@ __global__ void __launch_bounds__(64 * G * ((DUAL ? 2 : 1) + FP), 3) rx_kernel(
     const int grp0 = blockIdx.x * kGroups;
     for (int i = threadIdx.x; i < QK_FRAME / 2; i += kBlock)
         reinterpret_cast<float4*>(P)[i] = reinterpret_cast<const float4*>(a.ptab)[i];
-    qhunt::bconst_lds(threadIdx.x, kBlock, BT);
+    if constexpr ((MODE & 2) != 0) {
+        for (int i = threadIdx.x; i < kFftHT; i += kBlock) BT[i] = fft_tab[i];
+    } else {
+        qhunt::bconst_lds(threadIdx.x, kBlock, BT);
+    }
     if (wave < kGroups) {   // per-channel state of the groups at the call's first frame
         const int ch = (grp0 + wave) * W + lane;
         if (lane < W && ch < a.nch) {
@@ -899,9 +944,9 @@ __global__ void __launch_bounds__(64 * G * ((DUAL ? 2 : 1) + FP), 3) rx_kernel(
             const int ch0 = (grp0 + gi) * W + cbeg;
             const int nlive = max(0, min(kFrontCh, a.nch - ch0));
             float2* M = Ms[f];
-            int pf[kPf<MODE>];
+            int pf[kPf<DM>];
             if (((a.roles >> 4) & 3) == 1) __builtin_amdgcn_s_setprio(2);
-            if (nlive > 0) prefetch<MODE>(srcs(a, ch0, 0), lane, pf);
+            if (nlive > 0) prefetch<DM>(srcs(a, ch0, 0), lane, pf);
             for (int n = 0; n < a.F; n++) {
                 const int p = n & 1;
                 const unsigned g = a.g0 + (unsigned)n;
@@ -913,12 +958,12 @@ __global__ void __launch_bounds__(64 * G * ((DUAL ? 2 : 1) + FP), 3) rx_kernel(
                 for (int c = 0; c < nlive; c++) {
                     const int ch = ch0 + c;
                     float2* dcur = decs[f][c % kDecBuf];
-                    mix<MODE>(lane, pf, g, P, M);
+                    mix<DM>(lane, pf, g, P, M);
                     if (c > 0) store_window(lane, pmi, decs[f][(c - 1) % kDecBuf], wout + (size_t)(ch - 1) * kWinStride);
                     {
                         const bool same = c + 1 < nlive;
                         if (same || n + 1 < a.F)
-                            prefetch<MODE>(srcs(a, same ? ch + 1 : ch0, same ? n : n + 1), lane, pf);
+                            prefetch<DM>(srcs(a, same ? ch + 1 : ch0, same ? n : n + 1), lane, pf);
                     }
                     wave_lds_sync();
 #ifdef QPSK_STAMPS
@@ -931,7 +976,7 @@ __global__ void __launch_bounds__(64 * G * ((DUAL ? 2 : 1) + FP), 3) rx_kernel(
                 }
                 signal_add(&fcnt[gi][p], 1, lane);
             }
-            carry_history<MODE>(a.in, a.hist, a.F, ch0, nlive, lane);
+            carry_history<DM>(a.in, a.hist, a.F, ch0, nlive, lane);
         }
         __syncthreads();
         if (wave < kBackWaves && (wave & 1) == 0) {   // state after the call's last frame
@@ -983,10 +1028,10 @@ __global__ void __launch_bounds__(64 * G * ((DUAL ? 2 : 1) + FP), 3) rx_kernel(
         const int ch0 = (grp0 + gi) * QK_GROUP + cbeg;
         const int nlive = max(0, min(kFrontCh, a.nch - ch0));
         float2* M = Ms[f];
-        int pf[kPf<MODE>];
+        int pf[kPf<DM>];
         const bool on = (a.roles & 2) != 0 && nlive > 0;
         if (((a.roles >> 4) & 3) == 1) __builtin_amdgcn_s_setprio(2);
-        if (on) prefetch<MODE>(srcs(a, ch0, 0), lane, pf);
+        if (on) prefetch<DM>(srcs(a, ch0, 0), lane, pf);
         STAMP_DECL
         for (int n = 0; n < a.F; n++) {
             const int p = n & 1;
@@ -996,13 +1041,13 @@ __global__ void __launch_bounds__(64 * G * ((DUAL ? 2 : 1) + FP), 3) rx_kernel(
             for (int c = 0; on && c < nlive; c++) {
                 const int ch = ch0 + c;
                 float2* dcur = decs[f][c % kDecBuf];
-                mix<MODE>(lane, pf, g, P, M);
+                mix<DM>(lane, pf, g, P, M);
                 STAMP(0);
                 if (c > 0) store_window(lane, pmi, decs[f][(c - 1) % kDecBuf], wout + (size_t)(ch - 1) * kWinStride);
                 {   // next channel of this frame, else the first of the next frame
                     const bool same = c + 1 < nlive;
                     if (same || n + 1 < a.F)
-                        prefetch<MODE>(srcs(a, same ? ch + 1 : ch0, same ? n : n + 1), lane, pf);
+                        prefetch<DM>(srcs(a, same ? ch + 1 : ch0, same ? n : n + 1), lane, pf);
                 }
                 wave_lds_sync();
                 STAMP(1);
@@ -1016,7 +1061,7 @@ __global__ void __launch_bounds__(64 * G * ((DUAL ? 2 : 1) + FP), 3) rx_kernel(
             STAMP(7);
         }
         STAMP_FLUSH();
-        carry_history<MODE>(a.in, a.hist, a.F, ch0, nlive, lane);
+        carry_history<DM>(a.in, a.hist, a.F, ch0, nlive, lane);
     }
 }
 
@@ -1033,6 +1078,7 @@ float bits2f(uint32_t u) {
 struct qpsk_ctx {
     int device = 0, nch = 0, ngroup = 0;
     int mode = QPSK_MODE_REFERENCE;   // receiver semantics, fixed at creation
+    float* d_fft = nullptr;           // FFT-hunt tables (kFftHT floats), QPSK_MODE_FFT_HUNT
     uint64_t frames = 0;
     hipStream_t stream = nullptr;
     float2* d_ptab = nullptr;
@@ -1154,6 +1200,7 @@ static void ctx_free(qpsk_ctx* c) {
     (void)hipFree(c->d_njobs);
     (void)hipFree(c->d_ks);
     (void)hipFree(c->d_hist);
+    (void)hipFree(c->d_fft);
     for (int p = 0; p < 2; p++) {
         (void)hipFree(c->d_win[p]);
         (void)hipFree(c->d_mi[p]);
@@ -1167,6 +1214,35 @@ static void ctx_free(qpsk_ctx* c) {
     if (c->stream) (void)hipStreamDestroy(c->stream);
 }
 
+// The FFT hunt's LDS image (fft_hunt()): twiddles of fft_alloc(256, 0/1)
+// (src/fft.c:67-74, host C: qpsk_fft_host.c), Q = conj(fft(c)) with
+// c[i] = conj(preambletable[i]) for i < 128 (computed by the GPU FFT itself),
+// and kf_work's input permutation.
+static int fft_hunt_tables(qpsk_ctx* c) {
+    float tab[kFftHT];
+    qpsk_fft_twiddle_table(256, 0, tab);
+    qpsk_fft_twiddle_table(256, 1, tab + 512);
+    qpsk_fft_perm_table(256, reinterpret_cast<int*>(tab + 1536));
+    float cq[512] = {};
+    for (int i = 0; i < QK_NPRE; i++) {
+        cq[2 * i] = (float)QK_PRE[i];
+        cq[2 * i + 1] = -(float)QK_PRE[i];
+    }
+    int r = QPSK_OK;
+    qpsk_fft_plan* plan = qpsk_fft_alloc(c->device, 256, 0, &r);
+    if (!plan) return r;
+    r = qpsk_fft(plan, cq, cq, 1);
+    qpsk_fft_free(plan);
+    if (r != QPSK_OK) return r;
+    for (int k = 0; k < 256; k++) {
+        tab[1024 + 2 * k] = cq[2 * k];
+        tab[1024 + 2 * k + 1] = -cq[2 * k + 1];
+    }
+    HCHECK(hipMalloc(&c->d_fft, sizeof tab));
+    HCHECK(hipMemcpy(c->d_fft, tab, sizeof tab, hipMemcpyHostToDevice));
+    return QPSK_OK;
+}
+
 extern "C" qpsk_ctx* qpsk_rx_create(int device, int nch, int* err) {
     return qpsk_rx_create_mode(device, nch, QPSK_MODE_REFERENCE, err);
 }
@@ -1174,7 +1250,7 @@ extern "C" qpsk_ctx* qpsk_rx_create(int device, int nch, int* err) {
 extern "C" qpsk_ctx* qpsk_rx_create_mode(int device, int nch, int mode, int* err) {
     int dummy;
     if (!err) err = &dummy;
-    if (nch < 1 || (mode != QPSK_MODE_REFERENCE && mode != QPSK_MODE_DEC752)) {
+    if (nch < 1 || mode < 0 || mode > (QPSK_MODE_DEC752 | QPSK_MODE_FFT_HUNT)) {
         *err = QPSK_EINVAL;
         return nullptr;
     }
@@ -1227,6 +1303,7 @@ extern "C" qpsk_ctx* qpsk_rx_create_mode(int device, int nch, int mode, int* err
         r = herr(hipMemcpy(c->d_ptab, ptab, sizeof ptab, hipMemcpyHostToDevice));
         if (r == QPSK_OK) r = herr(hipMemcpy(c->d_ks, ksf, sizeof ksf, hipMemcpyHostToDevice));
     }
+    if (r == QPSK_OK && (mode & QPSK_MODE_FFT_HUNT)) r = fft_hunt_tables(c);
     if (r == QPSK_OK) r = qpsk_rx_reset(c);
     if (r != QPSK_OK) {
         ctx_free(c);
@@ -1300,7 +1377,7 @@ extern "C" int qpsk_rx_batch_device(qpsk_ctx* c, const int16_t* d_in, int F, uin
                        c->d_win[0], c->d_win[1], c->d_mi[0], c->d_mi[1], c->d_rt[0], c->d_rt[1], \
                        d_bits, d_valid, d_trace, reinterpret_cast<float2*>(d_soft), c->d_jobs,  \
                        c->d_njobs + parity, c->nch, F, (unsigned)(c->frames & 0xffffffffu),     \
-                       c->roles)
+                       c->roles, c->d_fft)
     // one group per workgroup: the dual-chain back (DUAL above) unless
     // QPSK_SHAPE=1x8s forces the single back wave
     // and the narrowest group width (64/32/16 channels) that still fits the
@@ -1325,8 +1402,12 @@ extern "C" int qpsk_rx_batch_device(qpsk_ctx* c, const int16_t* d_in, int F, uin
         else if (G == 2) QPSK_LAUNCH(2, 4, MM, false, 64);                                     \
         else QPSK_LAUNCH(4, 2, MM, false, 64);                                                 \
     } while (0)
-    if (c->mode == QPSK_MODE_DEC752) QPSK_LAUNCH_MODE(1);
-    else QPSK_LAUNCH_MODE(0);
+    switch (c->mode) {
+        case 0: QPSK_LAUNCH_MODE(0); break;
+        case 1: QPSK_LAUNCH_MODE(1); break;
+        case 2: QPSK_LAUNCH_MODE(2); break;
+        default: QPSK_LAUNCH_MODE(3); break;
+    }
 #undef QPSK_LAUNCH_MODE
 #undef QPSK_LAUNCH
     HCHECK(hipGetLastError());

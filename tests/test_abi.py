@@ -122,7 +122,7 @@ def test_create_mode_rejects_unknown_modes():
     """qpsk_rx_create_mode validates its arguments before touching a device."""
     import ctypes as C
     L = sc.lib()
-    for mode, nch in ((2, 4), (-1, 4), (sc.MODE_DEC752, 0)):
+    for mode, nch in ((4, 4), (-1, 4), (sc.MODE_DEC752, 0)):
         err = C.c_int(0)
         assert not L.qpsk_rx_create_mode(0, nch, mode, C.byref(err))
         assert err.value == -1   # QPSK_EINVAL

@@ -215,3 +215,58 @@ def test_fft_restatement_is_a_dft():
     x = (np.random.default_rng(3).standard_normal(256) * (1 + 1j)).astype(np.complex64)
     np.testing.assert_allclose(oracle.cpu_fft(x), np.fft.fft(x), atol=1e-4)
     np.testing.assert_allclose(oracle.cpu_fft(x, True), np.fft.ifft(x) * 256, atol=1e-4)
+
+
+# ------------------------------------------------------- FFT-correlation hunt
+# The QC_MODE_FFT_HUNT receiver variant replaces the hunt's direct sums by a
+# kiss_fft correlation.  The reference never calls its FFT, so no reference
+# build of this receiver exists; its hunt is pinned by composing the
+# reference's OWN fft() (oracle/_ref/libkissfft_ref.so) in numpy float32.
+PRE = np.array(json.load(open(os.path.join(os.path.dirname(__file__), "golden",
+                                           "fft_hunt_preamble.json"))), np.float32)
+
+
+def _hunt_with_reference_fft(dec):
+    c = np.zeros(256, np.complex64)
+    c.real[:128], c.imag[:128] = PRE, -PRE            # conj(preambletable[i])
+    C = oracle.ref_fft(c)
+    q_r, q_i = C.real, -C.imag                         # Q = conj(C)
+    X = oracle.ref_fft(np.asarray(dec, np.complex64)[:256])
+    y = np.empty(256, np.complex64)                    # (ac - bd, ad + bc) in float32
+    y.real = X.real * q_r - X.imag * q_i
+    y.imag = X.real * q_i + X.imag * q_r
+    S = oracle.ref_fft(y, True)[:128]
+    v = S.real * S.real + S.imag * S.imag              # cnormf, src/qpsk.c:75-80
+    best, mi = np.float32(0), 0
+    for l in range(128):                               # src/qpsk.c:172-183
+        if v[l] > best:
+            best, mi = v[l], l
+    return mi, q_r + 1j * q_i
+
+
+def test_fft_hunt_vs_reference_fft():
+    if not oracle.ref_fft_available():
+        pytest.skip("oracle/_ref not built (no /root/reference here)")
+    rng = np.random.default_rng(11)
+    for t in range(60):
+        dec = (rng.standard_normal(290) + 1j * rng.standard_normal(290)).astype(np.complex64)
+        if t % 3 == 0:   # a preamble at a random lag under noise
+            lag = int(rng.integers(0, 128))
+            dec[lag:lag + 128] += 3 * (PRE + 1j * PRE)
+        if t == 1:
+            dec[:] = 0
+        mi, q = _hunt_with_reference_fft(dec)
+        assert oracle.fft_hunt(dec) == mi, t
+    np.testing.assert_array_equal(oracle.fft_hunt_spectrum().view(np.uint32),
+                                  q.astype(np.complex64).view(np.uint32))
+
+
+def test_fft_hunt_mode_runs_and_is_the_direct_receiver_here():
+    """On the golden channels the FFT hunt picks the same lags as the direct
+    correlator (its rounding differs, its argmax does not), so the variant's
+    outputs equal the reference's there."""
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "synth_s3_eb4.npz"))
+    x = oracle.synth(int(g["seed"]), int(g["nch"]), int(g["nframes"]), float(g["ebn0_db"]))
+    bits, valid, tr = oracle.cpu_rx(x, trace=True, mode=oracle.MODE_FFT_HUNT)
+    np.testing.assert_array_equal(tr["max_index"], g["max_index"])
+    np.testing.assert_array_equal(np.packbits(bits, axis=-1), g["bits"])
