@@ -36,6 +36,9 @@ typedef struct qpsk_stream qpsk_stream;
 enum { QPSK_EBUSY = -4 };   /* acquire with every slot in flight: retrieve first */
 
 qpsk_stream *qpsk_stream_create(int device, int nch, int frames, int nslot, int *err);
+/* the same with the receiver semantics `mode` (QPSK_MODE_*, qpsk_batch.h) */
+qpsk_stream *qpsk_stream_create_mode(int device, int nch, int frames, int nslot, int mode,
+                                     int *err);
 void qpsk_stream_destroy(qpsk_stream *s);
 /* pinned input buffer of the next chunk, or NULL (*err = QPSK_EBUSY) */
 int16_t *qpsk_stream_acquire(qpsk_stream *s, int *err);

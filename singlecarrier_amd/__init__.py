@@ -90,6 +90,8 @@ def lib():
         L.qpsk_tx_phase_table.argtypes = [vp, C.c_long]
         L.qpsk_stream_create.restype = vp
         L.qpsk_stream_create.argtypes = [i32, i32, i32, i32, C.POINTER(C.c_int)]
+        L.qpsk_stream_create_mode.restype = vp
+        L.qpsk_stream_create_mode.argtypes = [i32, i32, i32, i32, i32, C.POINTER(C.c_int)]
         L.qpsk_stream_destroy.argtypes = [vp]
         L.qpsk_stream_acquire.restype = vp
         L.qpsk_stream_acquire.argtypes = [vp, C.POINTER(C.c_int)]
@@ -120,7 +122,7 @@ SYMBOLS = ["qpsk_rx_create", "qpsk_rx_create_mode", "qpsk_rx_mode", "qpsk_rx_des
            "qpsk_rx_init", "qpsk_tx_init", "qpsk_surface_error", "qpsk_tx_state_init",
            "qpsk_tx_frame_state", "qpsk_synth_batch", "qpsk_rx_timing_enable",
            "qpsk_rx_timing_collect", "qpsk_rx_timing_split", "qpsk_synth_device",
-           "qpsk_tx_phase_table", "qpsk_stream_create", "qpsk_stream_destroy",
+           "qpsk_tx_phase_table", "qpsk_stream_create", "qpsk_stream_create_mode", "qpsk_stream_destroy",
            "qpsk_stream_acquire", "qpsk_stream_submit", "qpsk_stream_pending",
            "qpsk_stream_retrieve", "qpsk_stream_ctx", "qpsk_records", "qpsk_fft_alloc",
            "qpsk_fft_free", "qpsk_fft_device", "qpsk_fft"]
@@ -236,9 +238,10 @@ class Stream:
     ``acquire()`` in place, ``submit()``, later ``retrieve()`` the oldest chunk.
     Every channel's state carries across chunks."""
 
-    def __init__(self, nch: int, frames: int, nslot: int = 3, device: int = 0):
+    def __init__(self, nch: int, frames: int, nslot: int = 3, device: int = 0,
+                 mode: int = MODE_REFERENCE):
         err = C.c_int(0)
-        self._h = lib().qpsk_stream_create(device, nch, frames, nslot, C.byref(err))
+        self._h = lib().qpsk_stream_create_mode(device, nch, frames, nslot, mode, C.byref(err))
         if not self._h:
             _check(err.value or -3)
         self.nch, self.frames, self.nslot = nch, frames, nslot

@@ -81,6 +81,11 @@ static int stream_alloc(qpsk_stream* s) {
 }
 
 extern "C" qpsk_stream* qpsk_stream_create(int device, int nch, int frames, int nslot, int* err) {
+    return qpsk_stream_create_mode(device, nch, frames, nslot, QPSK_MODE_REFERENCE, err);
+}
+
+extern "C" qpsk_stream* qpsk_stream_create_mode(int device, int nch, int frames, int nslot,
+                                                int mode, int* err) {
     int dummy;
     if (!err) err = &dummy;
     if (nch < 1 || frames < 1 || nslot < 1 || nslot > kMaxSlots) {
@@ -96,7 +101,7 @@ extern "C" qpsk_stream* qpsk_stream_create(int device, int nch, int frames, int 
     s->nch = nch;
     s->frames = frames;
     s->nslot = nslot;
-    s->rx = qpsk_rx_create(device, nch, err);
+    s->rx = qpsk_rx_create_mode(device, nch, mode, err);
     int r = s->rx ? stream_alloc(s) : *err;
     if (r != QPSK_OK) {
         stream_free(s);

@@ -83,3 +83,29 @@ def test_c_stream_driver(golden_dir, tmp_path):
         assert hashlib.md5(got0).hexdigest() == exp["output_md5"], fpc
         for i in range(3):
             assert open(f"{pre}{i + 1}.bin", "rb").read() == sc.records(bits[i], valid[i]), (fpc, i)
+
+
+@pytest.mark.parametrize("mode", [1, 3])
+def test_stream_in_variant_modes(mode):
+    """qpsk_stream_create_mode: the dec752 / FFT-hunt receivers behind the
+    streaming pipeline equal the oracle's same mode over the whole stream."""
+    nch, fpc, nchunk = 96, 3, 4
+    x = oracle.synth(18, nch, fpc * nchunk, 5.0)
+    eb, ev, _ = oracle.cpu_rx(x, mode=mode)
+    st = sc.Stream(nch, fpc, nslot=2, mode=mode)
+    got_b, got_v = [], []
+    for k in range(nchunk):
+        if st.pending == 2:
+            b, v = st.retrieve()
+            got_b.append(b)
+            got_v.append(v)
+        buf = st.acquire()
+        buf[...] = x[:, k * fpc:(k + 1) * fpc]
+        st.submit()
+    while st.pending:
+        b, v = st.retrieve()
+        got_b.append(b)
+        got_v.append(v)
+    st.close()
+    assert (np.concatenate(got_v, axis=1) == ev).all()
+    assert (np.concatenate(got_b, axis=1) == eb).all()
