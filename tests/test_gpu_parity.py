@@ -240,3 +240,21 @@ def test_exact_division_fallback(monkeypatch):
     monkeypatch.setenv("QPSK_FORCE_EXACT", "1")
     x = oracle.synth(63, 200, 10, 4.0)
     _vs_oracle(x)
+
+
+def test_long_stream_crosses_the_keystream_period():
+    """The descrambler's keystream repeats every 32,767 bits = 1,057 frames of 62
+    bits minus 1 (src/scramble.c: 15-bit LFSR); the GPU indexes it by the
+    global frame counter.  1,100 frames fed in uneven calls == the oracle."""
+    nch, nf = 48, 1100
+    x = oracle.synth(123, nch, nf, 1000.0)
+    bits, valid, _ = oracle.cpu_rx(x)
+    rx = sc.Receiver(nch)
+    outs, a = [], 0
+    for b in (300, 1, 499, 300):
+        outs.append(rx.demod(np.ascontiguousarray(x[:, a:a + b])))
+        a += b
+    assert rx.frames == nf
+    np.testing.assert_array_equal(np.concatenate([o["valid"] for o in outs], 1), valid)
+    np.testing.assert_array_equal(np.concatenate([o["bits"] for o in outs], 1), bits)
+    assert valid[:, 1057:].any()
