@@ -1038,6 +1038,12 @@ __global__ void __launch_bounds__(64 * G * ((DUAL ? 2 : 1) + FP), 3) rx_kernel(
             const unsigned g = a.g0 + (unsigned)n;
             float2* wout = win_of(a, g + 1u);
             int pmi = 0;
+            // roles bits 8-15 (QPSK_STAGGER): the second half of the front waves
+            // (the younger partner on each SIMD) starts each frame that many x
+            // 512 cycles late, so partners' FIR and MFMA/LDS phases interleave
+            // (MI355X_MICROARCH.md "two waves per SIMD", item 9)
+            for (int z = (f >= kFrontWaves / 2) ? (a.roles >> 8) & 255 : 0; z > 0; z--)
+                __builtin_amdgcn_s_sleep(8);
             for (int c = 0; on && c < nlive; c++) {
                 const int ch = ch0 + c;
                 float2* dcur = decs[f][c % kDecBuf];
@@ -1106,7 +1112,9 @@ struct qpsk_ctx {
     int ev_frames[kEv] = {};
     int ev_n = 0;
     bool timing = false;
-    int roles = 3 | (1 << 4);   // roles + priority; QPSK_ABLATE / QPSK_PRIO (profiling)
+    // roles + priority + front stagger (12 x 512 cycles: -0.7%, profiles/r01_stagger_ab.txt);
+    // QPSK_ABLATE / QPSK_PRIO / QPSK_STAGGER (profiling)
+    int roles = 3 | (1 << 4) | (12 << 8);
     int ncu = 256;              // compute units of the device
     int shape_groups = 0;       // 0: by batch size; QPSK_SHAPE (A/B experiments)
     bool single_back = false;   // QPSK_SHAPE=1x8s: G = 1 without the dual-chain back
@@ -1274,6 +1282,7 @@ extern "C" qpsk_ctx* qpsk_rx_create_mode(int device, int nch, int mode, int* err
         c->roles = (c->roles & 3) | (v << 4);
     }
     if (getenv("QPSK_FORCE_EXACT")) c->roles |= kForceExact;   // tests: exact-division path
+    if (const char* st = getenv("QPSK_STAGGER")) c->roles = (c->roles & ~(255 << 8)) | ((atoi(st) & 255) << 8);
     if (const char* w = getenv("QPSK_WIDTH")) {
         const int v = atoi(w);
         c->width = (v == 16 || v == 32 || v == 64) ? v : 0;
