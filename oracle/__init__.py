@@ -66,6 +66,8 @@ def cpu_lib():
         lib.qc_mixer_table.argtypes = [C.c_void_p]
         lib.qc_fft.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_void_p]
         lib.qc_fft_twiddles.argtypes = [C.c_int, C.c_int, C.c_void_p]
+        lib.qc_rx_stages.restype = C.c_long
+        lib.qc_rx_stages.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p]
         lib.qc_fft_hunt.restype = C.c_int
         lib.qc_fft_hunt.argtypes = [C.c_void_p]
         lib.qc_fft_hunt_spectrum.argtypes = [C.c_void_p]
@@ -282,3 +284,11 @@ def fft_hunt_spectrum() -> np.ndarray:
     q = np.empty(256, np.complex64)
     cpu_lib().qc_fft_hunt_spectrum(_p(q))
     return q
+
+
+def cpu_stages(x, mode: int = MODE_REF) -> np.ndarray:
+    """decimated_frame[0..289] after each call, one channel x [nframes][1880]."""
+    x = np.ascontiguousarray(x, dtype=np.int16).reshape(-1, FRAME)
+    dec = np.zeros((x.shape[0], 290, 2), np.float32)
+    cpu_lib().qc_rx_stages(_p(x), x.shape[0], mode, _p(dec))
+    return dec

@@ -264,8 +264,28 @@ static int data_eq(kal_t *k, const float (*x)[2], float soft[2]) {
     return (dI << 1) | dQ;
 }
 
+static int rx_frame(qc_chan_t *ch, const int16_t in[QC_FRAME], uint8_t bits[QC_BITS],
+                    qc_trace_t *tr, float (*dec_out)[2]);
+
 int qc_rx_frame(qc_chan_t *ch, const int16_t in[QC_FRAME], uint8_t bits[QC_BITS],
                 qc_trace_t *tr) {
+    return rx_frame(ch, in, bits, tr, NULL);
+}
+
+long qc_rx_stages(const int16_t *in, int nframes, int mode, float *dec_out) {
+    qc_chan_t *ch = (qc_chan_t *)malloc(sizeof(qc_chan_t));
+    uint8_t bits[QC_BITS];
+    long nvalid = 0;
+    qc_chan_init_mode(ch, mode);
+    for (int n = 0; n < nframes; n++)
+        nvalid += rx_frame(ch, in + (size_t)n * QC_FRAME, bits, NULL,
+                           (float (*)[2])(dec_out + (size_t)n * QC_DEC752 * 2));
+    free(ch);
+    return nvalid;
+}
+
+static int rx_frame(qc_chan_t *ch, const int16_t in[QC_FRAME], uint8_t bits[QC_BITS],
+                    qc_trace_t *tr, float (*dec_out)[2]) {
     const uint32_t n = ch->frame;
     const int rt = ch->rx_timing;
     const int d752 = (ch->mode & QC_MODE_DEC752) != 0;
@@ -294,6 +314,8 @@ int qc_rx_frame(qc_chan_t *ch, const int16_t in[QC_FRAME], uint8_t bits[QC_BITS]
         for (int j = 0; j < 102; j++) fir_at(M + j - LO, dec[QC_DEC + j]);
         for (int i = 0; i < QC_DEC; i++) fir_at(M + 5 * i + rt - LO, ch->dprev[i]);
     }
+
+    if (dec_out) memcpy(dec_out, dec, sizeof dec);   /* decimated_frame[0..289] */
 
     /* preamble hunt, src/qpsk.c:172-183 */
     int mi = 0;

@@ -69,6 +69,10 @@ int qc_rx_frame(qc_chan_t *ch, const int16_t in[QC_FRAME], uint8_t bits[QC_BITS]
  * tr [nch][nframes] or NULL.  Returns the number of valid frames. */
 long qc_rx_batch(const int16_t *in, int nch, int nframes, uint8_t *bits,
                  uint8_t *valid, qc_trace_t *tr, int nthreads);
+/* Stage tap: one channel from a fresh state; dec_out [nframes][290][2] gets
+ * the observable decimated_frame[0..289] of every call (after decimation,
+ * before the hunt), as the reference's buffer holds it.  Returns #valid. */
+long qc_rx_stages(const int16_t *in, int nframes, int mode, float *dec_out);
 /* Same, with the receiver semantics `mode` (QC_MODE_*). */
 long qc_rx_batch_mode(const int16_t *in, int nch, int nframes, uint8_t *bits,
                       uint8_t *valid, qc_trace_t *tr, int nthreads, int mode);

@@ -270,3 +270,23 @@ def test_fft_hunt_mode_runs_and_is_the_direct_receiver_here():
     bits, valid, tr = oracle.cpu_rx(x, trace=True, mode=oracle.MODE_FFT_HUNT)
     np.testing.assert_array_equal(tr["max_index"], g["max_index"])
     np.testing.assert_array_equal(np.packbits(bits, axis=-1), g["bits"])
+
+
+def test_decimated_frame_kat(golden_dir):
+    """Stage KAT: the restatement's decimated_frame[0..289] after
+    every call on the sample capture equals the reference's own buffer
+    (tests/golden/sample_stages.npz, from oracle/_ref), bit for bit.  This
+    pins the mixer, the RRC FIR and the model-A decimation separately from
+    the decisions."""
+    st = np.load(os.path.join(golden_dir, "sample_stages.npz"))
+    dec = oracle.cpu_stages(_sample(golden_dir)[0])
+    np.testing.assert_array_equal(dec.view(np.uint32), st["dec"].view(np.uint32))
+
+
+def test_decimated_frame_dec752_vs_padded_reference():
+    if not oracle.ref_available(oracle.MODE_DEC752):
+        pytest.skip("oracle/_ref not built (no /root/reference here)")
+    x = oracle.synth(77, 1, 12, 4.0)[0]
+    ref_dec = oracle.ref_stages(x, mode=oracle.MODE_DEC752)[0]
+    dec = oracle.cpu_stages(x, mode=oracle.MODE_DEC752)
+    np.testing.assert_array_equal(dec.view(np.uint32), ref_dec.view(np.uint32))
