@@ -940,9 +940,18 @@ __global__ void __launch_bounds__(64 * G * ((DUAL ? 2 : 1) + FP), 3) rx_kernel(
             // ---------------------------------------------------- front
             const int f = wave - kBackWaves;
             const int gi = f / kFrontPer;
-            const int cbeg = (f % kFrontPer) * kFrontCh;
+            const int fl = f % kFrontPer;
+            // roles bits 16-19 (QPSK_SPLIT = s, one group per workgroup only):
+            // the front waves that share a SIMD with a back wave (waves 4, 5,
+            // 8, 9 when waves map to SIMDs by wave % 4) take s channels fewer,
+            // the others s more
+            const int split = kGroups == 1 ? (a.roles >> 16) & 15 : 0;
+            auto share = [&](int x) { return ((x + kBackWaves) & 3) < kBackWaves; };
+            int cbeg = 0;
+            for (int x = 0; x < fl; x++) cbeg += kFrontCh + (share(x) ? -split : split);
+            const int mych = kFrontCh + (share(fl) ? -split : split);
             const int ch0 = (grp0 + gi) * W + cbeg;
-            const int nlive = max(0, min(kFrontCh, a.nch - ch0));
+            const int nlive = max(0, min(mych, a.nch - ch0));
             float2* M = Ms[f];
             int pf[kPf<DM>];
             if (((a.roles >> 4) & 3) == 1) __builtin_amdgcn_s_setprio(2);
@@ -1122,6 +1131,7 @@ struct qpsk_ctx {
     bool dual_multi = false;    // QPSK_SHAPE=4x1d: dual-chain backs, 4 groups x 1 front (A/B);
                                 // a 4x2 dual shape would need <= 128 VGPRs and spills
     bool single2 = false;       // QPSK_SHAPE=2x4: 2 groups without the dual-chain backs
+    bool tuned_split = false;   // QPSK_SPLIT / QPSK_PRIO given: no per-shape defaults
     float pend_ms[2] = {0.0f, 0.0f};
     int pend_frames = 0;
 };
@@ -1278,10 +1288,15 @@ extern "C" qpsk_ctx* qpsk_rx_create_mode(int device, int nch, int mode, int* err
         else if (!strcmp(ab, "back")) c->roles = (c->roles & ~3) | 1;
     }
     if (const char* pr = getenv("QPSK_PRIO")) {     // issue-priority experiments
+        c->tuned_split = true;
         const int v = !strcmp(pr, "front") ? 1 : !strcmp(pr, "back") ? 2 : 0;
         c->roles = (c->roles & 3) | (v << 4);
     }
     if (getenv("QPSK_FORCE_EXACT")) c->roles |= kForceExact;   // tests: exact-division path
+    if (const char* sp = getenv("QPSK_SPLIT")) {
+        c->roles |= (atoi(sp) & 15) << 16;
+        c->tuned_split = true;
+    }
     if (const char* st = getenv("QPSK_STAGGER")) c->roles = (c->roles & ~(255 << 8)) | ((atoi(st) & 255) << 8);
     if (const char* w = getenv("QPSK_WIDTH")) {
         const int v = atoi(w);
@@ -1386,7 +1401,7 @@ extern "C" int qpsk_rx_batch_device(qpsk_ctx* c, const int16_t* d_in, int F, uin
                        c->d_win[0], c->d_win[1], c->d_mi[0], c->d_mi[1], c->d_rt[0], c->d_rt[1], \
                        d_bits, d_valid, d_trace, reinterpret_cast<float2*>(d_soft), c->d_jobs,  \
                        c->d_njobs + parity, c->nch, F, (unsigned)(c->frames & 0xffffffffu),     \
-                       c->roles, c->d_fft)
+                       roles, c->d_fft)
     // one group per workgroup: the dual-chain back (DUAL above) unless
     // QPSK_SHAPE=1x8s forces the single back wave
     // and the narrowest group width (64/32/16 channels) that still fits the
@@ -1400,6 +1415,12 @@ extern "C" int qpsk_rx_batch_device(qpsk_ctx* c, const int16_t* d_in, int F, uin
         W = c->width > 0 ? c->width
           : (size_t)c->nch <= (size_t)16 * c->ncu ? 16 : (size_t)c->nch <= (size_t)32 * c->ncu ? 32 : 64;
     }
+    // 1x8 dual at W = 64 (8k-16k channels): back-wave priority and 2 channels
+    // moved off each front wave that shares a SIMD with a back wave (-3%,
+    // profiles/r01_split_ab.txt); the narrower widths keep front priority
+    int roles = c->roles;
+    if (dual && W == 64 && !c->tuned_split)
+        roles = (roles & ~((3 << 4) | (15 << 16))) | (2 << 4) | (2 << 16);
 #define QPSK_LAUNCH_MODE(MM)                                                                   \
     do {                                                                                       \
         if (dual_multi && G == 4) QPSK_LAUNCH(4, 1, MM, true, 64);                             \

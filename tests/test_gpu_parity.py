@@ -232,6 +232,15 @@ def test_dual_chain_group_widths(width, monkeypatch):
     _vs_oracle(x)
 
 
+@pytest.mark.parametrize("split", ["0", "3"])
+def test_dual_chain_uneven_front_split(split, monkeypatch):
+    """QPSK_SPLIT moves channels between the dual kernel's front waves (the
+    W = 64 default uses 2); every split covers each channel exactly once."""
+    monkeypatch.setenv("QPSK_WIDTH", "64")
+    monkeypatch.setenv("QPSK_SPLIT", split)
+    _vs_oracle(oracle.synth(65, 200, 9, 4.0))
+
+
 def test_exact_division_fallback(monkeypatch):
     """The Kalman step's fast reciprocal has an exact-division fallback that
     recomputes a whole frame (rx_kernel) or job (rx_data_kernel) when an
