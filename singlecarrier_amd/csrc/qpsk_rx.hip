@@ -1351,6 +1351,42 @@ extern "C" int qpsk_rx_channels(const qpsk_ctx* c) { return c ? c->nch : 0; }
 extern "C" int qpsk_rx_mode(const qpsk_ctx* c) { return c ? c->mode : QPSK_EINVAL; }
 extern "C" uint64_t qpsk_rx_frames(const qpsk_ctx* c) { return c ? c->frames : 0; }
 
+// The rx_kernel instantiation for a call (DESIGN.md "Kernels"):
+//   > 2 groups per CU (C3's 65,536 channels): 4x2, one back wave per group;
+//   2 groups per CU: 2x4 with dual-chain backs (11% faster at 32,768 channels,
+//     profiles/r01_dual_ab.txt);
+//   1 group per CU: 1x8 dual-chain, at the narrowest group width (16/32/64
+//     channels) that still fits the batch in one wave of workgroups; at
+//     W = 64 with back priority and 2 channels moved off each front wave that
+//     shares a SIMD with a back wave (-3%, profiles/r01_split_ab.txt).
+// QPSK_SHAPE (4x2 | 4x1d | 2x4 | 2x4d | 1x8 | 1x8s), QPSK_WIDTH, QPSK_SPLIT
+// and QPSK_PRIO override for A/B runs.
+struct Shape {
+    enum Kind { k4x2, k4x1d, k2x4, k2x4d, k1x8, k1x8d16, k1x8d32, k1x8d64 } kind;
+    int roles;
+};
+
+static Shape pick_shape(const qpsk_ctx* c) {
+    const int G = c->shape_groups > 0 ? c->shape_groups
+                : c->ngroup <= c->ncu ? 1 : c->ngroup <= 2 * c->ncu ? 2 : 4;
+    Shape sh{Shape::k4x2, c->roles};
+    if (G == 4) {
+        sh.kind = c->dual_multi ? Shape::k4x1d : Shape::k4x2;
+    } else if (G == 2) {
+        sh.kind = c->single2 ? Shape::k2x4 : Shape::k2x4d;
+    } else if (c->single_back) {
+        sh.kind = Shape::k1x8;
+    } else {
+        const int W = c->width > 0 ? c->width
+                    : (size_t)c->nch <= (size_t)16 * c->ncu ? 16
+                    : (size_t)c->nch <= (size_t)32 * c->ncu ? 32 : 64;
+        sh.kind = W == 16 ? Shape::k1x8d16 : W == 32 ? Shape::k1x8d32 : Shape::k1x8d64;
+        if (W == 64 && !c->tuned_split)
+            sh.roles = (sh.roles & ~((3 << 4) | (15 << 16))) | (2 << 4) | (2 << 16);
+    }
+    return sh;
+}
+
 // rx_data_kernel grid: persistent, 4 workgroups of 256 per CU
 static constexpr int kDataBlocks = 1024, kDataThreads = 256;
 
@@ -1389,48 +1425,27 @@ extern "C" int qpsk_rx_batch_device(qpsk_ctx* c, const int16_t* d_in, int F, uin
         c->ev_frames[slot] = F;
     }
     const int parity = (int)(c->calls & 1u);
-    // workgroup shape: the fewest groups per workgroup that still fit the
-    // batch in one wave of workgroups (QPSK_SHAPE=4x2|2x4|1x8 overrides)
-    const int G = c->shape_groups > 0 ? c->shape_groups
-                : c->ngroup <= c->ncu ? 1 : c->ngroup <= 2 * c->ncu ? 2 : 4;
+    const Shape sh = pick_shape(c);
 #define QPSK_LAUNCH(GG, FF, MM, DD, WW)                                                        \
     hipLaunchKernelGGL((rx_kernel<GG, FF, MM, DD, WW>),                                        \
                        dim3((unsigned)((c->nch + (size_t)GG * WW - 1) / ((size_t)GG * WW))),   \
                        dim3(64 * GG * ((DD ? 2 : 1) + FF)), 0, s, d_in, c->d_hist, c->d_ptab,  \
-                       c->d_ks,                                                                \
-                       c->d_win[0], c->d_win[1], c->d_mi[0], c->d_mi[1], c->d_rt[0], c->d_rt[1], \
-                       d_bits, d_valid, d_trace, reinterpret_cast<float2*>(d_soft), c->d_jobs,  \
-                       c->d_njobs + parity, c->nch, F, (unsigned)(c->frames & 0xffffffffu),     \
-                       roles, c->d_fft)
-    // one group per workgroup: the dual-chain back (DUAL above) unless
-    // QPSK_SHAPE=1x8s forces the single back wave
-    // and the narrowest group width (64/32/16 channels) that still fits the
-    // batch in one wave of workgroups (QPSK_WIDTH overrides)
-    const bool dual = G == 1 && !c->single_back;
-    // two groups per workgroup: dual-chain backs too (2x4d; 11% faster at
-    // 32,768 channels, profiles/r01_dual_ab.txt) unless QPSK_SHAPE=2x4
-    const bool dual_multi = (c->dual_multi && G == 4) || (G == 2 && !c->single2);
-    int W = 64;
-    if (dual) {
-        W = c->width > 0 ? c->width
-          : (size_t)c->nch <= (size_t)16 * c->ncu ? 16 : (size_t)c->nch <= (size_t)32 * c->ncu ? 32 : 64;
-    }
-    // 1x8 dual at W = 64 (8k-16k channels): back-wave priority and 2 channels
-    // moved off each front wave that shares a SIMD with a back wave (-3%,
-    // profiles/r01_split_ab.txt); the narrower widths keep front priority
-    int roles = c->roles;
-    if (dual && W == 64 && !c->tuned_split)
-        roles = (roles & ~((3 << 4) | (15 << 16))) | (2 << 4) | (2 << 16);
+                       c->d_ks, c->d_win[0], c->d_win[1], c->d_mi[0], c->d_mi[1], c->d_rt[0],  \
+                       c->d_rt[1], d_bits, d_valid, d_trace, reinterpret_cast<float2*>(d_soft), \
+                       c->d_jobs, c->d_njobs + parity, c->nch, F,                               \
+                       (unsigned)(c->frames & 0xffffffffu), sh.roles, c->d_fft)
 #define QPSK_LAUNCH_MODE(MM)                                                                   \
     do {                                                                                       \
-        if (dual_multi && G == 4) QPSK_LAUNCH(4, 1, MM, true, 64);                             \
-        else if (dual_multi) QPSK_LAUNCH(2, 4, MM, true, 64);                                  \
-        else if (dual && W == 16) QPSK_LAUNCH(1, 8, MM, true, 16);                             \
-        else if (dual && W == 32) QPSK_LAUNCH(1, 8, MM, true, 32);                             \
-        else if (dual) QPSK_LAUNCH(1, 8, MM, true, 64);                                        \
-        else if (G == 1) QPSK_LAUNCH(1, 8, MM, false, 64);                                     \
-        else if (G == 2) QPSK_LAUNCH(2, 4, MM, false, 64);                                     \
-        else QPSK_LAUNCH(4, 2, MM, false, 64);                                                 \
+        switch (sh.kind) {                                                                     \
+            case Shape::k4x1d: QPSK_LAUNCH(4, 1, MM, true, 64); break;                         \
+            case Shape::k2x4d: QPSK_LAUNCH(2, 4, MM, true, 64); break;                         \
+            case Shape::k1x8d16: QPSK_LAUNCH(1, 8, MM, true, 16); break;                       \
+            case Shape::k1x8d32: QPSK_LAUNCH(1, 8, MM, true, 32); break;                       \
+            case Shape::k1x8d64: QPSK_LAUNCH(1, 8, MM, true, 64); break;                       \
+            case Shape::k1x8: QPSK_LAUNCH(1, 8, MM, false, 64); break;                         \
+            case Shape::k2x4: QPSK_LAUNCH(2, 4, MM, false, 64); break;                         \
+            default: QPSK_LAUNCH(4, 2, MM, false, 64); break;                                  \
+        }                                                                                      \
     } while (0)
     switch (c->mode) {
         case 0: QPSK_LAUNCH_MODE(0); break;
