@@ -1132,6 +1132,7 @@ struct qpsk_ctx {
                                 // a 4x2 dual shape would need <= 128 VGPRs and spills
     bool single2 = false;       // QPSK_SHAPE=2x4: 2 groups without the dual-chain backs
     bool tuned_split = false;   // QPSK_SPLIT / QPSK_PRIO given: no per-shape defaults
+    int data_grid = 1024, data_block = 256;   // rx_data_kernel launch (QPSK_DATA_GRID/BLOCK)
     float pend_ms[2] = {0.0f, 0.0f};
     int pend_frames = 0;
 };
@@ -1293,6 +1294,9 @@ extern "C" qpsk_ctx* qpsk_rx_create_mode(int device, int nch, int mode, int* err
         c->roles = (c->roles & 3) | (v << 4);
     }
     if (getenv("QPSK_FORCE_EXACT")) c->roles |= kForceExact;   // tests: exact-division path
+    if (const char* g = getenv("QPSK_DATA_GRID")) c->data_grid = atoi(g) > 0 ? atoi(g) : 1024;
+    if (const char* b = getenv("QPSK_DATA_BLOCK"))
+        c->data_block = (atoi(b) >= 64 && atoi(b) <= 256 && atoi(b) % 64 == 0) ? atoi(b) : 256;
     if (const char* sp = getenv("QPSK_SPLIT")) {
         c->roles |= (atoi(sp) & 15) << 16;
         c->tuned_split = true;
@@ -1387,8 +1391,8 @@ static Shape pick_shape(const qpsk_ctx* c) {
     return sh;
 }
 
-// rx_data_kernel grid: persistent, 4 workgroups of 256 per CU
-static constexpr int kDataBlocks = 1024, kDataThreads = 256;
+// rx_data_kernel grid: persistent, 4 workgroups of 256 per CU (qpsk_ctx::data_grid/block;
+// other geometries measured within 2%, profiles/r01_data_ab.txt)
 
 extern "C" int qpsk_rx_batch_device(qpsk_ctx* c, const int16_t* d_in, int F, uint8_t* d_bits,
                                     uint8_t* d_valid, int32_t* d_trace, float* d_soft,
@@ -1457,7 +1461,7 @@ extern "C" int qpsk_rx_batch_device(qpsk_ctx* c, const int16_t* d_in, int F, uin
 #undef QPSK_LAUNCH
     HCHECK(hipGetLastError());
     if (slot >= 0) HCHECK(hipEventRecord(c->ev[slot][1], s));
-    hipLaunchKernelGGL(rx_data_kernel, dim3(kDataBlocks), dim3(kDataThreads), 0, s, c->d_jobs,
+    hipLaunchKernelGGL(rx_data_kernel, dim3(c->data_grid), dim3(c->data_block), 0, s, c->d_jobs,
                        c->d_njobs, c->d_ks, d_bits, reinterpret_cast<float2*>(d_soft), parity,
                        c->roles & kForceExact);
     HCHECK(hipGetLastError());
