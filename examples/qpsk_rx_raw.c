@@ -4,10 +4,12 @@
  *
  *   qpsk_rx_raw in.raw out.bin            single channel, qpsk_rx_frame() per frame
  *                                          (unchanged reference call pattern)
- *   qpsk_rx_raw -b in1.raw [in2.raw ...] -o PREFIX
+ *   qpsk_rx_raw -b [-m MODE] in1.raw [in2.raw ...] -o PREFIX
  *                                          every file is one channel; all channels are
  *                                          demodulated together through qpsk_rx_batch()
- *                                          and PREFIX<i>.bin is written per channel
+ *                                          and PREFIX<i>.bin is written per channel;
+ *                                          MODE = QPSK_MODE_* (qpsk_batch.h, default 0:
+ *                                          the reference; 1 dec752, 2 FFT hunt, 3 both)
  * Output: one 496-byte record per valid frame, bits in bytes 0..61 (the
  * reference's /tmp/databits.txt format, src/qpsk.c:455-457).
  * Build: gcc -O2 -Iinclude qpsk_rx_raw.c -Lsinglecarrier_amd -lqpsk_hip -Wl,-rpath,...
@@ -59,7 +61,7 @@ static int single(const char *in, const char *out) {
     return 0;
 }
 
-static int batch(int nch, char **paths, const char *prefix) {
+static int batch(int nch, char **paths, const char *prefix, int mode) {
     int nf = -1;
     int16_t **ch = calloc((size_t)nch, sizeof(int16_t *));
     for (int c = 0; c < nch; c++) {
@@ -74,7 +76,7 @@ static int batch(int nch, char **paths, const char *prefix) {
         memcpy(in + (size_t)c * nf * FRAME_SIZE, ch[c], sizeof(int16_t) * (size_t)nf * FRAME_SIZE);
     uint8_t *bits = malloc((size_t)nch * nf * 62), *valid = malloc((size_t)nch * nf);
     int err;
-    qpsk_ctx *ctx = qpsk_rx_create(0, nch, &err);
+    qpsk_ctx *ctx = qpsk_rx_create_mode(0, nch, mode, &err);
     if (!ctx) {
         fprintf(stderr, "qpsk: %s\n", qpsk_strerror(err));
         return 3;
@@ -104,8 +106,15 @@ static int batch(int nch, char **paths, const char *prefix) {
 
 int main(int argc, char **argv) {
     if (argc >= 3 && strcmp(argv[1], "-b") != 0) return single(argv[1], argv[2]);
-    if (argc >= 5 && !strcmp(argv[1], "-b") && !strcmp(argv[argc - 2], "-o"))
-        return batch(argc - 4, argv + 2, argv[argc - 1]);
-    fprintf(stderr, "usage: %s in.raw out.bin | -b in1.raw [in2.raw ...] -o PREFIX\n", argv[0]);
+    if (argc >= 5 && !strcmp(argv[1], "-b") && !strcmp(argv[argc - 2], "-o")) {
+        int first = 2, mode = QPSK_MODE_REFERENCE;
+        if (argc >= 7 && !strcmp(argv[2], "-m")) {
+            mode = atoi(argv[3]);
+            first = 4;
+        }
+        return batch(argc - 2 - first, argv + first, argv[argc - 1], mode);
+    }
+    fprintf(stderr, "usage: %s in.raw out.bin | -b [-m MODE] in1.raw [in2.raw ...] -o PREFIX\n",
+            argv[0]);
     return 2;
 }

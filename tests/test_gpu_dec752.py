@@ -132,3 +132,16 @@ def test_full_size_c3():
     np.testing.assert_array_equal(out["bits"], bits)
     np.testing.assert_array_equal(out["trace"][..., 3], tr["rx_timing"])
     np.testing.assert_array_equal(out["trace"][..., 0], tr["max_index"])
+
+
+def test_c_driver_mode_flag(golden_dir, tmp_path):
+    """examples/qpsk_rx_raw.c -b -m 1: the dec752 receiver from C gives the
+    padded reference build's output file for the sample capture."""
+    import subprocess
+    exe = os.path.abspath(os.path.join(golden_dir, "..", "..", "examples", "qpsk_rx_raw"))
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-s", "-C", os.path.dirname(exe)], check=True)
+    raw = os.path.join(golden_dir, "preamble_qpsk_8k.raw")
+    subprocess.run([exe, "-b", "-m", "1", raw, "-o", str(tmp_path / "d")], check=True)
+    exp = json.load(open(os.path.join(golden_dir, "sample_expected_dec752.json")))
+    assert hashlib.md5((tmp_path / "d0.bin").read_bytes()).hexdigest() == exp["output_md5"]
