@@ -145,6 +145,20 @@ __device__ __forceinline__ void spin_wait(int* p, int v) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
+// spin_wait that reports a timeout (the flow kernel's front waves stop waiting
+// after one, so a logic error costs 0.1 s per wave, not per channel)
+__device__ __forceinline__ bool spin_wait_b(int* p, int v) {
+    bool ok = false;
+    for (unsigned it = 0; it < (1u << 22); it++) {
+        const int c = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+        if (c >= v) { ok = true; break; }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    return ok;
+}
+
 // publish: every earlier store of this wave (LDS and global) is visible to the
 // workgroup before the counter moves
 __device__ __forceinline__ void signal_set(int* p, int v, int lane) {
@@ -786,6 +800,176 @@ __device__ __forceinline__ void back_frame(const RxArgs& a, int ch, bool live, i
     }
 }
 
+// ------------------------------------------------------------ flow back wave
+// rx_kernel<.., FLOW = true>: lane = channel, and every lane runs its own
+// frames.  The frame decision (src/qpsk.c:196: valid iff matches > 98) is
+// settled once 30 of the 128 training steps have missed; the rest of such a
+// frame's training is unobservable (an invalid frame outputs zeros and keeps
+// rx_timing), so the lane finishes it there and starts its next frame while
+// its neighbours are still training.  Per-channel LDS counters replace the
+// per-frame barrier: fdone[c] = fronts finished for channel c (window n and
+// mi_n ready when fdone >= n), bdone[c] = frames decided (rt_n ready when
+// bdone >= n).  The trace (tests) reports matches of all 128 steps, so a traced
+// call, or roles bit kNoEarly, trains every frame to the end.
+constexpr int kNoEarly = 1 << 20;     // roles bit (QPSK_EARLY=0)
+constexpr int kMissMax = QK_NPRE - QK_MATCH_MIN;   // 30 misses: matches <= 98, invalid
+
+// 4 x train_eq from slot i + 1 (i % 4 == 0, per lane); nib = preamble bits i..i+3
+template <bool EXACT>
+__device__ __forceinline__ void train4(Kal& k, f2 (&x)[5], const f2* wp2, int i, unsigned nib,
+                                       int& matches, bool& bad) {
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+        const f2 nx = wp2[i + t + 6];
+        const float ref = ((nib >> t) & 1u) ? 1.0f : -1.0f;
+        f2 v = {0.0f, 0.0f};
+#pragma unroll
+        for (int s = 0; s < 5; s++) v = v + cmul(x[s], k.eq[s]);
+        const float er = ref - v.x;
+        update_eq<EXACT>(k, x, f2{er, v.y}, bad);
+        if (er * ref > 0.0f) matches++;
+#pragma unroll
+        for (int s = 0; s < 4; s++) x[s] = x[s + 1];
+        x[4] = nx;
+    }
+}
+
+__device__ __forceinline__ int lds_load(const int* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+__device__ __forceinline__ f2 sel(bool c, f2 a, f2 b) { return f2{c ? a.x : b.x, c ? a.y : b.y}; }
+
+// the lane id, recomputed where used (volatile: not hoisted into a register that
+// lives across the training steps)
+__device__ __forceinline__ int lane_fresh() {
+    int l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
+
+// One back wave of the flow kernel: group channels ch0 + lane (lane < nlive).
+// mi / rt: the group's mi_s / rt_s [parity][lane]; fdone / bdone per lane.
+// The training steps run on every lane of the wave under uniform control flow
+// (a lane without a frame computes on stale state and its results are never
+// used), so the equalizer state has one home in registers; lanes start a frame
+// by select, not by branch.  A lane whose fast-reciprocal operands left their
+// range (`bad`) trains the frame again with IEEE division; while one does, the
+// whole wave takes the exact step, which equals the fast one on in-range lanes.
+__device__ __forceinline__ void back_flow(const RxArgs& a, int ch0, int nlive, int (*mi)[QK_GROUP],
+                                          int (*rt)[QK_GROUP], int* fdone, int* bdone,
+                                          const unsigned char* nibs) {
+    const int lane = lane_id();
+    const int ch = ch0 + lane;
+    const bool early = a.trace == nullptr && (a.roles & kNoEarly) == 0;
+    const bool force = (a.roles & kForceExact) != 0;
+    int n = lane < nlive ? 0 : a.F;    // this lane's frame
+    bool act = false, bad = false, exact = false;
+    int i = 0, matches = 0;
+    Kal k = kal_reset();
+    // a lane without a frame reads the group's first window (always in bounds)
+    const f2* wp2 = reinterpret_cast<const f2*>(win_of(a, a.g0) + (size_t)ch0 * kWinStride);
+    f2 x[5];
+    load_x0(reinterpret_cast<const float4*>(wp2), x);
+    for (unsigned idle = 0; idle < (1u << 22);) {   // ~0.1 s with every lane waiting: a logic error
+        // idle lanes with a frame left start it once its window is there
+        const bool want = !act && n < a.F;
+        if (__ballot(want)) {
+            const bool go = want && lds_load(fdone + lane_fresh()) >= n;
+            if (__ballot(go)) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                int chl = ch;
+                asm volatile("" : "+v"(chl));   // no per-lane address hoisted out of the loop
+                const f2* nw = reinterpret_cast<const f2*>(win_of(a, a.g0 + (unsigned)min(n, a.F - 1)) +
+                                                           (size_t)chl * kWinStride);
+                wp2 = go ? nw : wp2;
+                const Kal r = kal_reset();
+#pragma unroll
+                for (int t = 0; t < 5; t++) {
+                    k.eq[t] = sel(go, r.eq[t], k.eq[t]);
+                    k.d[t] = sel(go, r.d[t], k.d[t]);
+                }
+#pragma unroll
+                for (int t = 0; t < 10; t++) k.u[t] = sel(go, r.u[t], k.u[t]);
+                f2 x0[5];
+                load_x0(reinterpret_cast<const float4*>(wp2), x0);
+#pragma unroll
+                for (int t = 0; t < 5; t++) x[t] = sel(go, x0[t], x[t]);
+                i = go ? 0 : i;
+                matches = go ? 0 : matches;
+                bad = go ? force && !exact : bad;
+                act = act || go;
+            }
+        }
+        if (__ballot(act) == 0ull) {
+            if (__ballot(n < a.F) == 0ull) break;
+            __builtin_amdgcn_s_sleep(1);
+            idle++;
+            continue;
+        }
+        idle = 0;
+        {
+            const unsigned nib = nibs[i >> 2];   // preamble bits i..i+3 (LDS)
+            if (__ballot(act && exact)) train4<true>(k, x, wp2, i, nib, matches, bad);
+            else train4<false>(k, x, wp2, i, nib, matches, bad);
+            i += act ? 4 : 0;   // a lane without a frame stays inside its window
+        }
+        const bool fin = act && (i == QK_NPRE || (early && i - matches >= kMissMax));
+        if (__ballot(fin) == 0ull) continue;
+        if (fin && bad && !exact) {   // train the frame again, exactly
+            exact = true;
+            act = false;
+        }
+        const bool done = fin && act;
+        if (__ballot(done) == 0ull) continue;
+        if (done) {
+            const int lane = lane_fresh();
+            const bool valid = matches > QK_MATCH_MIN;
+            int chl = ch;
+            asm volatile("" : "+v"(chl));   // no per-lane address hoisted out of the loop
+            const size_t cf = (size_t)chl * a.F + n;
+            // mi_n and rt_n stay in LDS during the training (register pressure);
+            // the front rewrites neither before this frame is decided
+            const int mi_n = mi[n & 1][lane];
+            int rt_n = rt[n & 1][lane];
+            const unsigned long long vm = __ballot(valid);   // finishing lanes only
+            if (vm) {
+                const int first = __builtin_ctzll(__ballot(1));
+                unsigned base = 0;
+                if (lane == first) base = atomicAdd(a.njobs, (unsigned)__popcll(vm));
+                base = __shfl(base, first);
+                if (valid) {
+                    const unsigned slot = base + __builtin_amdgcn_mbcnt_hi(
+                        (unsigned)(vm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)vm, 0u));
+                    DataJob j;
+                    j.k = k;
+                    j.cf = cf;
+                    j.ks = (a.g0 + (unsigned)n) % QK_KS_FRAMES;
+                    put_job(a.jobs + (size_t)slot * kJobF4, j, wp2 + 129);
+                }
+            }
+            if (!valid) {   // invalid frame: bits (and soft symbols) are zero
+                uint16_t* bo = reinterpret_cast<uint16_t*>(a.bits + cf * QK_NBITS);
+                for (int ss = 0; ss < QK_NDSYM; ss++) bo[ss] = 0;
+                if (a.soft) {
+                    float2* so = a.soft + cf * QK_NDSYM;
+                    for (int ss = 0; ss < QK_NDSYM; ss++) so[ss] = make_float2(0.0f, 0.0f);
+                }
+            }
+            if (valid) rt_n = mi_n + QK_NPRE;   // src/qpsk.c:219
+            a.valid[cf] = valid ? 1 : 0;
+            if (a.trace)
+                *reinterpret_cast<int4*>(a.trace + cf * 4) = make_int4(mi_n, matches, valid ? 1 : 0, rt_n);
+            rt[(n + 1) & 1][lane] = rt_n;
+            n++;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __hip_atomic_store(bdone + lane, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            act = false;
+            exact = false;
+        }
+    }
+}
+
 // 31 x data_eq + qpsk_demod (src/equalizer.c:64-90, src/qpsk.c:268-271) from
 // the job's window samples xs; returns the raw dibits (bit 2s = Q, 2s+1 = I).
 // Decisions collect in a register; the caller stores the 62 bytes after the
@@ -871,7 +1055,10 @@ __global__ void __launch_bounds__(256) rx_data_kernel(const float4* jobs, unsign
 // W (DUAL only): channels per group, 64, 32 or 16.  A narrower group leaves
 // back lanes idle but spreads a small batch over more CUs and gives each front
 // wave fewer channels per frame, which shortens the front half of the chain.
-template <int G, int FP, int MODE, bool DUAL, int W = QK_GROUP>
+//
+// FLOW (not DUAL): back_flow() backs with early-terminated training and
+// per-channel progress counters instead of the per-frame __syncthreads().
+template <int G, int FP, int MODE, bool DUAL, int W = QK_GROUP, bool FLOW = false>
 __global__ void __launch_bounds__(64 * G * ((DUAL ? 2 : 1) + FP), 3) rx_kernel(
     const int16_t* in, int16_t* hist, const float2* ptab, const unsigned long long* ks,
     float2* win0, float2* win1, int* mi0, int* mi1, int* rt0, int* rt1, uint8_t* bits,
@@ -894,6 +1081,8 @@ __global__ void __launch_bounds__(64 * G * ((DUAL ? 2 : 1) + FP), 3) rx_kernel(
     // hunt tables: the MFMA correlator's B, or the FFT hunt's twiddles / Q / permutation
     __shared__ __attribute__((aligned(16))) float BT[(MODE & 2) ? kFftHT : qhunt::kBT];
     __shared__ int bseq[kGroups][2], fcnt[kGroups][2];   // DUAL progress counters, per group
+    __shared__ int fdone[FLOW ? kGroups : 1][QK_GROUP], bdone[FLOW ? kGroups : 1][QK_GROUP];   // FLOW
+    __shared__ unsigned char pre_nib[QK_NPRE / 4];   // FLOW: preamble bits 4i..4i+3
     const int lane = threadIdx.x & 63;
     // wave-uniform by construction; readfirstlane tells the compiler, so every
     // per-wave index and pointer below lives in SGPRs
@@ -914,7 +1103,99 @@ __global__ void __launch_bounds__(64 * G * ((DUAL ? 2 : 1) + FP), 3) rx_kernel(
         }
     }
     if (threadIdx.x < 2 * kGroups) (&bseq[0][0])[threadIdx.x] = (&fcnt[0][0])[threadIdx.x] = 0;
+    if constexpr (FLOW) {
+        for (int i = threadIdx.x; i < kGroups * QK_GROUP; i += kBlock)
+            (&fdone[0][0])[i] = (&bdone[0][0])[i] = 0;
+        if (threadIdx.x < QK_NPRE / 4)
+            pre_nib[threadIdx.x] = (unsigned char)(((threadIdx.x < 16 ? kPreLo : kPreHi) >> (4 * (threadIdx.x & 15))) & 15u);
+    }
     __syncthreads();
+    if constexpr (FLOW) {
+        static_assert(!DUAL, "flow kernel: one back wave per group");
+        if (wave < kGroups) {
+            const int gi = wave;
+            const int gch0 = (grp0 + gi) * QK_GROUP;
+            const int nl = max(0, min(QK_GROUP, a.nch - gch0));
+            if (((a.roles >> 4) & 3) == 2) __builtin_amdgcn_s_setprio(2);
+            if (nl > 0) back_flow(a, gch0, nl, mi_s[gi], rt_s[gi], fdone[gi], bdone[gi], pre_nib);
+        } else {
+            const int f = wave - kGroups;
+            const int gi = f / kFrontPer;
+            const int cbeg = (f % kFrontPer) * kFrontCh;
+            const int ch0 = (grp0 + gi) * QK_GROUP + cbeg;
+            const int nlive = max(0, min(kFrontCh, a.nch - ch0));
+            float2* M = Ms[f];
+            int pf[kPf<DM>];
+            if (((a.roles >> 4) & 3) == 1) __builtin_amdgcn_s_setprio(2);
+            if (nlive > 0) prefetch<DM>(srcs(a, ch0, 0), lane, pf);
+            // the younger front wave of each SIMD starts late once (QPSK_STAGGER)
+            for (int z = (f >= kFrontWaves / 2) ? (a.roles >> 8) & 255 : 0; z > 0; z--)
+                __builtin_amdgcn_s_sleep(8);
+            // windows stored and published to the back, in (frame, channel)
+            // order: npub windows published, the next is channel pc of frame pn.
+            // A window is published once a later vmcnt wait has covered its
+            // store (after the next channel's mix).
+            int nst = 0, npub = 0, pc = 0, pn = 0;
+            auto publish = [&] {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                for (; npub < nst; npub++) {
+                    if (lane == 0)
+                        __hip_atomic_store(&fdone[gi][cbeg + pc], pn + 1, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if (++pc == nlive) { pc = 0; pn++; }
+                }
+            };
+            bool dead = false;
+            for (int n = 0; n < a.F; n++) {
+                const int p = n & 1;
+                const unsigned g = a.g0 + (unsigned)n;
+                float2* wout = win_of(a, g + 1u);
+                int pmi = 0;
+                for (int c = 0; c < nlive; c++) {
+                    const int ch = ch0 + c;
+                    float2* dcur = decs[f][c % kDecBuf];
+                    mix<DM>(lane, pf, g, P, M);
+                    publish();
+                    if (c > 0) {
+                        store_window(lane, pmi, decs[f][(c - 1) % kDecBuf], wout + (size_t)(ch - 1) * kWinStride);
+                        nst++;
+                    }
+                    {
+                        const bool same = c + 1 < nlive;
+                        if (same || n + 1 < a.F)
+                            prefetch<DM>(srcs(a, same ? ch + 1 : ch0, same ? n : n + 1), lane, pf);
+                    }
+                    wave_lds_sync();
+                    // back(n-1) of this channel decided: rt_n, and window n+1's buffer
+                    // (window n-1) and mi_s[p ^ 1] (mi_{n-1}) are free
+                    if (n > 0 && !dead) dead = !spin_wait_b(&bdone[gi][cbeg + c], n);
+#ifdef QPSK_STAMPS
+                    unsigned long long st_acc[16];   // flow shapes are not stamped
+#endif
+                    pmi = front_channel<MODE>(lane, rt_s[gi][p][cbeg + c], M, dcur, BT FACC_ARG);
+                    if (lane == 0) mi_s[gi][p ^ 1][cbeg + c] = pmi;
+                    if (c + 1 == nlive) {
+                        store_window(lane, pmi, dcur, wout + (size_t)ch * kWinStride);
+                        nst++;
+                    }
+                    wave_lds_sync();
+                }
+            }
+            publish();
+            carry_history<DM>(a.in, a.hist, a.F, ch0, nlive, lane);
+        }
+        __syncthreads();
+        if (wave < kGroups) {   // state after the call's last frame
+            const int ch = (grp0 + wave) * QK_GROUP + lane;
+            if (ch < a.nch) {
+                const unsigned ge = a.g0 + (unsigned)a.F;
+                mi_of(a, ge)[ch] = mi_s[wave][a.F & 1][lane];
+                rt_of(a, ge)[ch] = rt_s[wave][a.F & 1][lane];
+            }
+        }
+        return;
+    }
     if constexpr (DUAL) {
         if (wave < kBackWaves) {
             // ---------------------------------------------------- back of group wave/2,
@@ -1131,6 +1412,7 @@ struct qpsk_ctx {
     bool dual_multi = false;    // QPSK_SHAPE=4x1d: dual-chain backs, 4 groups x 1 front (A/B);
                                 // a 4x2 dual shape would need <= 128 VGPRs and spills
     bool single2 = false;       // QPSK_SHAPE=2x4: 2 groups without the dual-chain backs
+    bool flow = false;          // QPSK_SHAPE=4x2f / 2x4f: flow backs (early-terminated training)
     bool tuned_split = false;   // QPSK_SPLIT / QPSK_PRIO given: no per-shape defaults
     int data_grid = 1024, data_block = 256;   // rx_data_kernel launch (QPSK_DATA_GRID/BLOCK)
     float pend_ms[2] = {0.0f, 0.0f};
@@ -1291,9 +1573,11 @@ extern "C" qpsk_ctx* qpsk_rx_create_mode(int device, int nch, int mode, int* err
     if (const char* pr = getenv("QPSK_PRIO")) {     // issue-priority experiments
         c->tuned_split = true;
         const int v = !strcmp(pr, "front") ? 1 : !strcmp(pr, "back") ? 2 : 0;
-        c->roles = (c->roles & 3) | (v << 4);
+        c->roles = (c->roles & ~(3 << 4)) | (v << 4);
     }
     if (getenv("QPSK_FORCE_EXACT")) c->roles |= kForceExact;   // tests: exact-division path
+    if (const char* e = getenv("QPSK_EARLY"))                   // flow shapes: 0 = train 128 steps
+        if (!strcmp(e, "0")) c->roles |= kNoEarly;
     if (const char* g = getenv("QPSK_DATA_GRID")) c->data_grid = atoi(g) > 0 ? atoi(g) : 1024;
     if (const char* b = getenv("QPSK_DATA_BLOCK"))
         c->data_block = (atoi(b) >= 64 && atoi(b) <= 256 && atoi(b) % 64 == 0) ? atoi(b) : 256;
@@ -1310,8 +1594,10 @@ extern "C" qpsk_ctx* qpsk_rx_create_mode(int device, int nch, int mode, int* err
     {
         c->shape_groups = !strcmp(sh, "1x8") || !strcmp(sh, "1x8s") ? 1
                         : !strcmp(sh, "2x4") || !strcmp(sh, "2x4d") ? 2
-                        : !strcmp(sh, "4x2") || !strcmp(sh, "4x1d") ? 4 : 0;
+                        : !strcmp(sh, "2x4f") ? 2
+                        : !strcmp(sh, "4x2") || !strcmp(sh, "4x1d") || !strcmp(sh, "4x2f") ? 4 : 0;
         c->dual_multi = !strcmp(sh, "4x1d");
+        c->flow = !strcmp(sh, "4x2f") || !strcmp(sh, "2x4f");
         c->single2 = !strcmp(sh, "2x4");
         c->single_back = !strcmp(sh, "1x8s");
     }
@@ -1363,10 +1649,11 @@ extern "C" uint64_t qpsk_rx_frames(const qpsk_ctx* c) { return c ? c->frames : 0
 //     channels) that still fits the batch in one wave of workgroups; at
 //     W = 64 with back priority and 2 channels moved off each front wave that
 //     shares a SIMD with a back wave (-3%, profiles/r01_split_ab.txt).
-// QPSK_SHAPE (4x2 | 4x1d | 2x4 | 2x4d | 1x8 | 1x8s), QPSK_WIDTH, QPSK_SPLIT
-// and QPSK_PRIO override for A/B runs.
+// QPSK_SHAPE (4x2 | 4x1d | 2x4 | 2x4d | 1x8 | 1x8s | 4x2f | 2x4f), QPSK_WIDTH,
+// QPSK_SPLIT and QPSK_PRIO override for A/B runs.  The flow shapes (f) are
+// exact but slower (DESIGN.md "Next" item 2, profiles/r01_flow_ab.txt).
 struct Shape {
-    enum Kind { k4x2, k4x1d, k2x4, k2x4d, k1x8, k1x8d16, k1x8d32, k1x8d64 } kind;
+    enum Kind { k4x2, k4x1d, k2x4, k2x4d, k1x8, k1x8d16, k1x8d32, k1x8d64, k4x2f, k2x4f } kind;
     int roles;
 };
 
@@ -1375,9 +1662,9 @@ static Shape pick_shape(const qpsk_ctx* c) {
                 : c->ngroup <= c->ncu ? 1 : c->ngroup <= 2 * c->ncu ? 2 : 4;
     Shape sh{Shape::k4x2, c->roles};
     if (G == 4) {
-        sh.kind = c->dual_multi ? Shape::k4x1d : Shape::k4x2;
+        sh.kind = c->dual_multi ? Shape::k4x1d : c->flow ? Shape::k4x2f : Shape::k4x2;
     } else if (G == 2) {
-        sh.kind = c->single2 ? Shape::k2x4 : Shape::k2x4d;
+        sh.kind = c->single2 ? Shape::k2x4 : c->flow ? Shape::k2x4f : Shape::k2x4d;
     } else if (c->single_back) {
         sh.kind = Shape::k1x8;
     } else {
@@ -1430,8 +1717,8 @@ extern "C" int qpsk_rx_batch_device(qpsk_ctx* c, const int16_t* d_in, int F, uin
     }
     const int parity = (int)(c->calls & 1u);
     const Shape sh = pick_shape(c);
-#define QPSK_LAUNCH(GG, FF, MM, DD, WW)                                                        \
-    hipLaunchKernelGGL((rx_kernel<GG, FF, MM, DD, WW>),                                        \
+#define QPSK_LAUNCH(GG, FF, MM, DD, WW, FL)                                                    \
+    hipLaunchKernelGGL((rx_kernel<GG, FF, MM, DD, WW, FL>),                                    \
                        dim3((unsigned)((c->nch + (size_t)GG * WW - 1) / ((size_t)GG * WW))),   \
                        dim3(64 * GG * ((DD ? 2 : 1) + FF)), 0, s, d_in, c->d_hist, c->d_ptab,  \
                        c->d_ks, c->d_win[0], c->d_win[1], c->d_mi[0], c->d_mi[1], c->d_rt[0],  \
@@ -1441,14 +1728,16 @@ extern "C" int qpsk_rx_batch_device(qpsk_ctx* c, const int16_t* d_in, int F, uin
 #define QPSK_LAUNCH_MODE(MM)                                                                   \
     do {                                                                                       \
         switch (sh.kind) {                                                                     \
-            case Shape::k4x1d: QPSK_LAUNCH(4, 1, MM, true, 64); break;                         \
-            case Shape::k2x4d: QPSK_LAUNCH(2, 4, MM, true, 64); break;                         \
-            case Shape::k1x8d16: QPSK_LAUNCH(1, 8, MM, true, 16); break;                       \
-            case Shape::k1x8d32: QPSK_LAUNCH(1, 8, MM, true, 32); break;                       \
-            case Shape::k1x8d64: QPSK_LAUNCH(1, 8, MM, true, 64); break;                       \
-            case Shape::k1x8: QPSK_LAUNCH(1, 8, MM, false, 64); break;                         \
-            case Shape::k2x4: QPSK_LAUNCH(2, 4, MM, false, 64); break;                         \
-            default: QPSK_LAUNCH(4, 2, MM, false, 64); break;                                  \
+            case Shape::k4x1d: QPSK_LAUNCH(4, 1, MM, true, 64, false); break;                  \
+            case Shape::k2x4d: QPSK_LAUNCH(2, 4, MM, true, 64, false); break;                  \
+            case Shape::k1x8d16: QPSK_LAUNCH(1, 8, MM, true, 16, false); break;                \
+            case Shape::k1x8d32: QPSK_LAUNCH(1, 8, MM, true, 32, false); break;                \
+            case Shape::k1x8d64: QPSK_LAUNCH(1, 8, MM, true, 64, false); break;                \
+            case Shape::k1x8: QPSK_LAUNCH(1, 8, MM, false, 64, false); break;                  \
+            case Shape::k2x4: QPSK_LAUNCH(2, 4, MM, false, 64, false); break;                  \
+            case Shape::k4x2f: QPSK_LAUNCH(4, 2, MM, false, 64, true); break;                  \
+            case Shape::k2x4f: QPSK_LAUNCH(2, 4, MM, false, 64, true); break;                  \
+            default: QPSK_LAUNCH(4, 2, MM, false, 64, false); break;                           \
         }                                                                                      \
     } while (0)
     switch (c->mode) {

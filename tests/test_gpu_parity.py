@@ -222,6 +222,66 @@ def test_every_workgroup_shape(shape, monkeypatch):
     _vs_oracle(x)
 
 
+def _vs_oracle_untraced(x, rx=None):
+    """No trace: the flow kernel's early-terminated training is on."""
+    rx = rx or sc.Receiver(x.shape[0])
+    out = rx.demod(x, soft=True)
+    bits, valid, tr = oracle.cpu_rx(x, trace=True)
+    np.testing.assert_array_equal(out["valid"], valid)
+    np.testing.assert_array_equal(out["bits"], bits)
+    vm = valid.astype(bool)
+    np.testing.assert_array_equal(out["soft"][vm], tr["soft"][vm])
+    assert not out["soft"][~vm].any()
+    return out, valid
+
+
+@pytest.mark.parametrize("shape", ["4x2f", "2x4f"])
+@pytest.mark.parametrize("ebn0", [1000.0, 3.0, 0.0])
+def test_flow_kernel_early_termination(shape, ebn0, monkeypatch):
+    """rx_kernel<.., FLOW>: every back lane runs its own frames and ends an
+    invalid frame's training after 30 misses.  Untraced (early termination on)
+    and traced (all 128 steps, matches in the trace) calls both equal the
+    oracle; the low-SNR batches mix valid and invalid frames on every lane."""
+    monkeypatch.setenv("QPSK_SHAPE", shape)
+    x = oracle.synth(71, 300, 12, ebn0)
+    _, valid = _vs_oracle_untraced(x)
+    if ebn0 < 10:   # the reference model leaves most low-SNR frames invalid
+        assert 0 < valid.sum() < valid.size
+    _vs_oracle(x)
+
+
+def test_flow_kernel_no_early(monkeypatch):
+    """QPSK_EARLY=0 trains every frame to the end (the A/B baseline)."""
+    monkeypatch.setenv("QPSK_SHAPE", "4x2f")
+    monkeypatch.setenv("QPSK_EARLY", "0")
+    _vs_oracle_untraced(oracle.synth(72, 257, 10, 2.0))
+
+
+def test_flow_kernel_exact_division(monkeypatch):
+    """The exact-division recompute inside a flow lane (all 128 steps)."""
+    monkeypatch.setenv("QPSK_SHAPE", "4x2f")
+    monkeypatch.setenv("QPSK_FORCE_EXACT", "1")
+    _vs_oracle_untraced(oracle.synth(73, 200, 8, 2.0))
+
+
+def test_flow_kernel_streaming_split(monkeypatch):
+    """rx_timing / max_index carried between flow calls: 1+4+2+9 frames == one call."""
+    monkeypatch.setenv("QPSK_SHAPE", "4x2f")
+    x = oracle.synth(74, 300, 16, 3.0)
+    rx = sc.Receiver(300)
+    parts = [rx.demod(np.ascontiguousarray(x[:, a:b]), soft=True)
+             for a, b in ((0, 1), (1, 5), (5, 7), (7, 16))]
+    bits, valid, _ = oracle.cpu_rx(x)
+    np.testing.assert_array_equal(np.concatenate([p["valid"] for p in parts], 1), valid)
+    np.testing.assert_array_equal(np.concatenate([p["bits"] for p in parts], 1), bits)
+
+
+def test_flow_kernel_full_size_c3(monkeypatch):
+    """65,536 channels x 16 frames at 3 dB through the flow kernel, untraced."""
+    monkeypatch.setenv("QPSK_SHAPE", "4x2f")
+    _vs_oracle_untraced(oracle.synth(75, 65536, 16, 3.0))
+
+
 @pytest.mark.parametrize("width", ["16", "32", "64"])
 def test_dual_chain_group_widths(width, monkeypatch):
     """One group per workgroup runs the dual-chain kernel (two back waves,
