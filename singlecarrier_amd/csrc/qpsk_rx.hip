@@ -95,6 +95,7 @@ struct RxArgs {
     unsigned* njobs;         // their count (this call's counter)
     int nch, F;
     unsigned g0;             // global index of the call's first frame
+    size_t jcap;             // job queue capacity (plane stride of the jobs)
     int roles;               // bit 0: back, bit 1: front (3 in production); bits 4-5:
                              // issue priority boost (0 none, 1 front, 2 back)
 };
@@ -633,7 +634,11 @@ __device__ __forceinline__ void update_eq(Kal& k, const f2 (&x)[5], f2 e, bool& 
 
 // A valid frame handed from the back wave to rx_data_kernel: the window
 // samples of its data symbols, the equalizer state after the 128 training
-// steps, and where its outputs go.  112 floats (28 x 16 B):
+// steps, and where its outputs go.  112 floats (28 x 16 B), plane-major: 16-B
+// word q of job slot s is at jobs[q * cap + s] (cap = the queue's capacity), so
+// the lanes of a wave, which hold consecutive slots, read and write adjacent
+// 16-B words (one uncoalesced 448-B job per lane touched 64 cache lines per
+// load instruction):
 //   [0, 70)  x = dec[mi+128+t], t < 35, as (re, im)
 //   [70, 80) eq[5]   [80, 100) u[10]   [100, 105) d[5] (one copy of each)
 //   [105, 107) cf (channel-frame index, 64-bit)   [107] keystream frame index
@@ -661,19 +666,27 @@ __device__ __forceinline__ float job_word(int i, const DataJob& j, const float* 
 // Streamed: each 16-B store right after the window loads it needs (the job
 // queue may alias the window as far as the compiler knows, so staging the
 // whole job first would hold all 112 floats in registers).
-__device__ __forceinline__ void put_job(float4* out, const DataJob& j, const f2* x35) {
+// Addresses: plane base (wave-uniform, SGPRs) + 32-bit lane byte offset slot * 16
+// (global_load/store saddr form; the queue holds < 2^28 jobs, qpsk_rx_batch_device).
+__device__ __forceinline__ const char* job_plane(const float4* jobs, size_t cap, int q) {
+    return reinterpret_cast<const char*>(jobs) + (size_t)q * cap * sizeof(float4);
+}
+
+__device__ __forceinline__ void put_job(float4* jobs, size_t cap, unsigned slot, const DataJob& j,
+                                        const f2* x35) {
     const float* xf = reinterpret_cast<const float*>(x35);
+    const unsigned off = slot * (unsigned)sizeof(float4);
 #pragma unroll
     for (int q = 0; q < kJobF4; q++)
-        out[q] = make_float4(job_word(4 * q, j, xf), job_word(4 * q + 1, j, xf),
+        *reinterpret_cast<float4*>(const_cast<char*>(job_plane(jobs, cap, q)) + off) = make_float4(job_word(4 * q, j, xf), job_word(4 * q + 1, j, xf),
                              job_word(4 * q + 2, j, xf), job_word(4 * q + 3, j, xf));
 }
 
-__device__ __forceinline__ void get_job(const float4* in, DataJob& j) {
+__device__ __forceinline__ void get_job(const float4* jobs, size_t cap, unsigned off, DataJob& j) {
     float v[112];
 #pragma unroll
     for (int q = 17; q < kJobF4; q++) {   // floats 68..111 (state and indices)
-        const float4 w = in[q];
+        const float4 w = *reinterpret_cast<const float4*>(job_plane(jobs, cap, q) + off);
         v[4 * q] = w.x; v[4 * q + 1] = w.y; v[4 * q + 2] = w.z; v[4 * q + 3] = w.w;
     }
 #pragma unroll
@@ -779,7 +792,7 @@ __device__ __forceinline__ void back_frame(const RxArgs& a, int ch, bool live, i
             j.k = k;
             j.cf = cf;
             j.ks = (a.g0 + (unsigned)n) % QK_KS_FRAMES;
-            put_job(a.jobs + (size_t)slot * kJobF4, j, wp2 + 129);
+            put_job(a.jobs, a.jcap, slot, j, wp2 + 129);
         }
     }
     if (live && !valid) {   // invalid frame: bits (and soft symbols) are zero
@@ -945,7 +958,7 @@ __device__ __forceinline__ void back_flow(const RxArgs& a, int ch0, int nlive, i
                     j.k = k;
                     j.cf = cf;
                     j.ks = (a.g0 + (unsigned)n) % QK_KS_FRAMES;
-                    put_job(a.jobs + (size_t)slot * kJobF4, j, wp2 + 129);
+                    put_job(a.jobs, a.jcap, slot, j, wp2 + 129);
                 }
             }
             if (!valid) {   // invalid frame: bits (and soft symbols) are zero
@@ -974,8 +987,18 @@ __device__ __forceinline__ void back_flow(const RxArgs& a, int ch0, int nlive, i
 // the job's window samples xs; returns the raw dibits (bit 2s = Q, 2s+1 = I).
 // Decisions collect in a register; the caller stores the 62 bytes after the
 // loop, so no wait on a store sits inside it.
+// the job's window samples: x[t] is float2 (t & 1) of 16-B word t >> 1
+struct JobX {
+    const float4* jobs;
+    size_t cap;
+    unsigned off;   // slot * 16
+    __device__ __forceinline__ f2 operator[](int t) const {
+        return *reinterpret_cast<const f2*>(job_plane(jobs, cap, t >> 1) + off + 8u * (t & 1));
+    }
+};
+
 template <bool EXACT>
-__device__ __forceinline__ unsigned long long data_steps(Kal& k, f2 (&x)[5], const f2* xs,
+__device__ __forceinline__ unsigned long long data_steps(Kal& k, f2 (&x)[5], const JobX xs,
                                                          float2* so, bool& bad) {
     unsigned long long dib = 0;
     for (int s = 0; s < QK_NDSYM; s++) {
@@ -1003,17 +1026,19 @@ __device__ __forceinline__ unsigned long long data_steps(Kal& k, f2 (&x)[5], con
 // lanes for 31 of its 159 steps.  Jobs come from the call's rx_kernel in any
 // order; every output location is fixed by the job, so results do not depend
 // on it.
-__global__ void __launch_bounds__(256) rx_data_kernel(const float4* jobs, unsigned* njobs,
+__global__ void __launch_bounds__(256) rx_data_kernel(const float4* jobs, unsigned long long jcap,
+                                                      unsigned* njobs,
                                                       const unsigned long long* ks_tab,
                                                       uint8_t* bits, float2* soft, int parity,
                                                       int force_exact) {
+    const size_t cap = (size_t)jcap;
     const unsigned n = njobs[parity];
     const unsigned stride = gridDim.x * blockDim.x;
     for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        const float4* jp = jobs + (size_t)i * kJobF4;
+        const unsigned off = i * (unsigned)sizeof(float4);
         DataJob j;
-        get_job(jp, j);
-        const f2* xs = reinterpret_cast<const f2*>(jp);   // x = dec[mi+128+t], t < 35
+        get_job(jobs, cap, off, j);
+        const JobX xs{jobs, cap, off};   // x = dec[mi+128+t], t < 35
         f2 x[5];
 #pragma unroll
         for (int t = 0; t < 5; t++) x[t] = xs[t];
@@ -1022,7 +1047,7 @@ __global__ void __launch_bounds__(256) rx_data_kernel(const float4* jobs, unsign
         bool bad = force_exact != 0;
         unsigned long long dib = data_steps<false>(j.k, x, xs, so, bad);
         if (__builtin_expect(bad, 0)) {   // recompute the job with IEEE division
-            get_job(jp, j);
+            get_job(jobs, cap, off, j);
 #pragma unroll
             for (int t = 0; t < 5; t++) x[t] = xs[t];
             dib = data_steps<true>(j.k, x, xs, so, bad);
@@ -1063,7 +1088,7 @@ __global__ void __launch_bounds__(64 * G * ((DUAL ? 2 : 1) + FP), 3) rx_kernel(
     const int16_t* in, int16_t* hist, const float2* ptab, const unsigned long long* ks,
     float2* win0, float2* win1, int* mi0, int* mi1, int* rt0, int* rt1, uint8_t* bits,
     uint8_t* valid, int32_t* trace, float2* soft, float4* jobs, unsigned* njobs, int nch, int F,
-    unsigned g0, int roles, const float* fft_tab) {
+    unsigned g0, int roles, const float* fft_tab, unsigned long long jcap) {
     static_assert(W == QK_GROUP || (DUAL && G == 1 && W % FP == 0 && W <= QK_GROUP), "group width");
     constexpr int kGroups = G, kFrontPer = FP;
     constexpr int kBackWaves = DUAL ? 2 * kGroups : kGroups;
@@ -1071,7 +1096,7 @@ __global__ void __launch_bounds__(64 * G * ((DUAL ? 2 : 1) + FP), 3) rx_kernel(
     constexpr int kFrontWaves = kGroups * kFrontPer;
     constexpr int kBlock = 64 * (kBackWaves + kFrontWaves);
     const RxArgs a{in, hist, ptab, ks, win0, win1, mi0, mi1, rt0, rt1, bits, valid, trace, soft,
-                   jobs, njobs, nch, F, g0, roles};
+                   jobs, njobs, nch, F, g0, (size_t)jcap, roles};
     __shared__ __attribute__((aligned(16))) float2 P[QK_FRAME];
     constexpr int DM = MODE & 1;   // decimation semantics; MODE & 2: FFT hunt
     constexpr int kM = Cfg<DM>::kM, kDecBuf = Cfg<DM>::kDecBuf;
@@ -1690,6 +1715,9 @@ extern "C" int qpsk_rx_batch_device(qpsk_ctx* c, const int16_t* d_in, int F, uin
     HCHECK(hipSetDevice(c->device));
     hipStream_t s = (hipStream_t)stream;
     const size_t need = (size_t)c->nch * (size_t)F;   // every frame valid, at most
+    // job slots are addressed with 32-bit byte offsets (slot * 16); 2^28 channel-
+    // frames would be 1 TB of input, beyond any device's memory
+    if (need >= ((size_t)1 << 28)) return QPSK_EINVAL;
     if (need > c->jobs_cap) {
         HCHECK(hipDeviceSynchronize());   // an earlier call may still use the queue
         (void)hipFree(c->d_jobs);
@@ -1724,7 +1752,8 @@ extern "C" int qpsk_rx_batch_device(qpsk_ctx* c, const int16_t* d_in, int F, uin
                        c->d_ks, c->d_win[0], c->d_win[1], c->d_mi[0], c->d_mi[1], c->d_rt[0],  \
                        c->d_rt[1], d_bits, d_valid, d_trace, reinterpret_cast<float2*>(d_soft), \
                        c->d_jobs, c->d_njobs + parity, c->nch, F,                               \
-                       (unsigned)(c->frames & 0xffffffffu), sh.roles, c->d_fft)
+                       (unsigned)(c->frames & 0xffffffffu), sh.roles, c->d_fft,                \
+                       (unsigned long long)c->jobs_cap)
 #define QPSK_LAUNCH_MODE(MM)                                                                   \
     do {                                                                                       \
         switch (sh.kind) {                                                                     \
@@ -1751,8 +1780,8 @@ extern "C" int qpsk_rx_batch_device(qpsk_ctx* c, const int16_t* d_in, int F, uin
     HCHECK(hipGetLastError());
     if (slot >= 0) HCHECK(hipEventRecord(c->ev[slot][1], s));
     hipLaunchKernelGGL(rx_data_kernel, dim3(c->data_grid), dim3(c->data_block), 0, s, c->d_jobs,
-                       c->d_njobs, c->d_ks, d_bits, reinterpret_cast<float2*>(d_soft), parity,
-                       c->roles & kForceExact);
+                       (unsigned long long)c->jobs_cap, c->d_njobs, c->d_ks, d_bits,
+                       reinterpret_cast<float2*>(d_soft), parity, c->roles & kForceExact);
     HCHECK(hipGetLastError());
     if (slot >= 0) HCHECK(hipEventRecord(c->ev[slot][2], s));
     c->frames += (uint64_t)F;
