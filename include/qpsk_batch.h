@@ -38,7 +38,8 @@ typedef struct qpsk_ctx qpsk_ctx;
 
 enum {
     QPSK_OK = 0,
-    QPSK_EINVAL = -1,     /* bad argument (NULL ctx/in, nch < 1, nframes < 0) */
+    QPSK_EINVAL = -1,     /* bad argument (NULL ctx/in, nch < 1, nframes < 0,
+                             nch * nframes >= 2^28 in one call: 1 TB of input) */
     QPSK_ENOMEM = -2,     /* device or host allocation failed */
     QPSK_ENODEV = -3,     /* no such HIP device */
     QPSK_EHIP = -1000,    /* QPSK_EHIP - hipError_t */
