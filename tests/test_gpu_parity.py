@@ -327,3 +327,18 @@ def test_long_stream_crosses_the_keystream_period():
     np.testing.assert_array_equal(np.concatenate([o["valid"] for o in outs], 1), valid)
     np.testing.assert_array_equal(np.concatenate([o["bits"] for o in outs], 1), bits)
     assert valid[:, 1057:].any()
+
+
+def test_per_call_job_limit():
+    """The data-job queue is addressed with 32-bit byte offsets: a call of
+    nch * nframes >= 2^28 channel-frames (1 TB of input) is refused with
+    QPSK_EINVAL before any device work (include/qpsk_batch.h)."""
+    import ctypes as C
+    rx = sc.Receiver(65536)
+    L = sc.lib()
+    fake = C.c_void_p(1 << 20)   # 16-B aligned, never dereferenced
+    r = L.qpsk_rx_batch_device(rx._h, fake, 4096, fake, fake, None, None, None)
+    assert r == -1
+    # the context is still usable
+    x = oracle.synth(76, 65536, 1, 1000.0)
+    np.testing.assert_array_equal(rx.demod(x)["bits"], oracle.cpu_rx(x)[0])
