@@ -342,3 +342,24 @@ def test_per_call_job_limit():
     # the context is still usable
     x = oracle.synth(76, 65536, 1, 1000.0)
     np.testing.assert_array_equal(rx.demod(x)["bits"], oracle.cpu_rx(x)[0])
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_random_batches_and_splits(seed):
+    """Seeded random shapes: channel count (ragged groups, every shape the
+    batch size selects), frame count, Eb/N0 and how the frames are split over
+    calls; everything (bits, flags, trace, soft) equals the oracle."""
+    rng = np.random.default_rng(900 + seed)
+    nch = int(rng.choice([1, 17, 64, 200, 777, 3000, 16500, 40000]))
+    nf = int(rng.integers(2, 12))
+    ebn0 = float(rng.choice([1000.0, 8.0, 4.0, 1.0]))
+    x = oracle.synth(1000 + seed, nch, nf, ebn0)
+    bits, valid, tr = oracle.cpu_rx(x, trace=True)
+    cuts = sorted(set(int(c) for c in rng.integers(1, nf, size=2)))
+    rx = sc.Receiver(nch)
+    parts, a = [], 0
+    for b in cuts + [nf]:
+        parts.append(rx.demod(np.ascontiguousarray(x[:, a:b]), trace=True, soft=True))
+        a = b
+    out = {k: np.concatenate([p[k] for p in parts], axis=1) for k in ("bits", "valid", "trace", "soft")}
+    _assert_same(out, bits, valid, tr)
