@@ -1617,12 +1617,12 @@ extern "C" qpsk_ctx* qpsk_rx_create_mode(int device, int nch, int mode, int* err
     }
     if (const char* sh = getenv("QPSK_SHAPE"))
     {
-        c->shape_groups = !strcmp(sh, "1x8") || !strcmp(sh, "1x8s") ? 1
+        c->shape_groups = !strcmp(sh, "1x8") || !strcmp(sh, "1x8s") || !strcmp(sh, "1x8f") ? 1
                         : !strcmp(sh, "2x4") || !strcmp(sh, "2x4d") ? 2
                         : !strcmp(sh, "2x4f") ? 2
                         : !strcmp(sh, "4x2") || !strcmp(sh, "4x1d") || !strcmp(sh, "4x2f") ? 4 : 0;
         c->dual_multi = !strcmp(sh, "4x1d");
-        c->flow = !strcmp(sh, "4x2f") || !strcmp(sh, "2x4f");
+        c->flow = !strcmp(sh, "4x2f") || !strcmp(sh, "2x4f") || !strcmp(sh, "1x8f");
         c->single2 = !strcmp(sh, "2x4");
         c->single_back = !strcmp(sh, "1x8s");
     }
@@ -1674,11 +1674,11 @@ extern "C" uint64_t qpsk_rx_frames(const qpsk_ctx* c) { return c ? c->frames : 0
 //     channels) that still fits the batch in one wave of workgroups; at
 //     W = 64 with back priority and 2 channels moved off each front wave that
 //     shares a SIMD with a back wave (-3%, profiles/r01_split_ab.txt).
-// QPSK_SHAPE (4x2 | 4x1d | 2x4 | 2x4d | 1x8 | 1x8s | 4x2f | 2x4f), QPSK_WIDTH,
+// QPSK_SHAPE (4x2 | 4x1d | 2x4 | 2x4d | 1x8 | 1x8s | 4x2f | 2x4f | 1x8f), QPSK_WIDTH,
 // QPSK_SPLIT and QPSK_PRIO override for A/B runs.  The flow shapes (f) are
 // exact but slower (DESIGN.md "Next" item 2, profiles/r01_flow_ab.txt).
 struct Shape {
-    enum Kind { k4x2, k4x1d, k2x4, k2x4d, k1x8, k1x8d16, k1x8d32, k1x8d64, k4x2f, k2x4f } kind;
+    enum Kind { k4x2, k4x1d, k2x4, k2x4d, k1x8, k1x8d16, k1x8d32, k1x8d64, k4x2f, k2x4f, k1x8f } kind;
     int roles;
 };
 
@@ -1692,6 +1692,8 @@ static Shape pick_shape(const qpsk_ctx* c) {
         sh.kind = c->single2 ? Shape::k2x4 : c->flow ? Shape::k2x4f : Shape::k2x4d;
     } else if (c->single_back) {
         sh.kind = Shape::k1x8;
+    } else if (c->flow) {
+        sh.kind = Shape::k1x8f;
     } else {
         const int W = c->width > 0 ? c->width
                     : (size_t)c->nch <= (size_t)16 * c->ncu ? 16
@@ -1766,6 +1768,7 @@ extern "C" int qpsk_rx_batch_device(qpsk_ctx* c, const int16_t* d_in, int F, uin
             case Shape::k2x4: QPSK_LAUNCH(2, 4, MM, false, 64, false); break;                  \
             case Shape::k4x2f: QPSK_LAUNCH(4, 2, MM, false, 64, true); break;                  \
             case Shape::k2x4f: QPSK_LAUNCH(2, 4, MM, false, 64, true); break;                  \
+            case Shape::k1x8f: QPSK_LAUNCH(1, 8, MM, false, 64, true); break;                  \
             default: QPSK_LAUNCH(4, 2, MM, false, 64, false); break;                           \
         }                                                                                      \
     } while (0)
