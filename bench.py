@@ -3,11 +3,15 @@
 
 One "step" = demodulating one batch: every channel of the workload advances by
 `--frames` 1880-sample frames (C3: 65536 channels x 32 frames = 3.94e9 int16
-samples, 7.88 GB, resident in HBM before timing).  Channels are independent,
-so N GPUs each take their own 65536-channel shard (distinct channels, no
-collective; "scaling": "weak"; --strong splits one 65536-channel batch).
+samples, 7.88 GB, resident in HBM before timing).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+N GPUs (C4): the 65536-channel batch is split into N channel
+shards, shard g = channels [g*C/N, (g+1)*C/N) on GPU g, one process per GPU,
+no collective on the data path ("scaling": "strong"; --weak gives every GPU
+its own 65536-channel batch instead).  The barrier around the timed region and
+the MAX-over-ranks time reduction run over gloo on the host, not RCCL.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]     (spawns N ranks itself)
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
 Rank 0 prints ONE JSON line.  See DESIGN.md "Measurement" for every field.
@@ -29,8 +33,8 @@ METRIC = "demodulated Msamples/sec (whole node), 65536-channel 8 kHz batch; BER 
 FRAME = 1880
 ALG_BYTES_PER_FRAME = 3760 + 63     # int16 in + 62 bit-bytes + valid byte
 HBM_PEAK_GBS = 8000.0               # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-VALU_PEAK_TOPS = 78.6               # fp32 non-FMA lane-ops/s: 256 CU x 128 lanes x 2.4 GHz
-OPS_PER_SAMPLE_MIN = 96.0           # minimal bit-exact formulation
+VALU_SIMDS = 256 * 4                 # MI355X: 256 CUs x 4 SIMD-32
+VALU_CLOCK_GHZ = 2.4                 # max engine clock (MI355X_MICROARCH.md)
 
 
 # receiver semantics (include/qpsk_batch.h QPSK_MODE_*): reference parity, the
@@ -38,27 +42,77 @@ OPS_PER_SAMPLE_MIN = 96.0           # minimal bit-exact formulation (SURVEY.md 8
 MODES = {"reference": 0, "dec752": 1, "fft": 2, "dec752fft": 3}
 
 
-def shard(channels: int, world: int, rank: int, strong: bool):
-    """(channels on this rank, first global channel id).  Weak: every rank
-    demodulates its own `channels`-channel batch (distinct channel ids); strong:
-    one `channels`-channel batch is split across the ranks."""
+def shard(channels: int, world: int, rank: int, strong: bool = True):
+    """(channels on this rank, first global channel id).  Strong (C4, default):
+    one `channels`-channel batch split across the ranks, shard g = channels
+    [g*C/N, (g+1)*C/N) (src/qpsk.c:436-458 is the per-channel
+    loop being split); weak: every rank demodulates its own `channels`-channel
+    batch (distinct channel ids)."""
     if strong:
         base, rem = divmod(channels, world)
         return base + (1 if rank < rem else 0), rank * base + min(rank, rem)
     return channels, rank * channels
 
 
-def reduce_step(dist, wall: float, nch: int, device):
-    """Job time = MAX over ranks of the timed region; channels = SUM."""
+def reduce_step(dist, wall: float, nch: int):
+    """Job time = MAX over ranks of the timed region; channels = SUM.  Host
+    tensors over the gloo group: no collective touches the GPUs."""
     import torch
     if dist is None:
         return wall, nch
-    t = torch.tensor([wall, float(nch)], dtype=torch.float64, device=device)
-    tmax = t[:1].clone()
+    tmax = torch.tensor([wall], dtype=torch.float64)
     dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-    tot = t[1:].clone()
+    tot = torch.tensor([nch], dtype=torch.int64)
     dist.all_reduce(tot)
     return float(tmax.item()), int(tot.item())
+
+
+def free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch(nproc: int, argv, script: str = None, env=None) -> int:
+    """Run `script argv` as `nproc` ranks (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_*
+    as torch.distributed.run sets them), one per GPU, and wait for all of
+    them.  The launcher itself makes no GPU call (children are started before
+    anything here touches HIP, and by Popen, never exec).  Returns the worst
+    exit status."""
+    import subprocess
+    script = script or os.path.abspath(__file__)
+    port = free_port()
+    procs = []
+    for r in range(nproc):
+        e = dict(os.environ if env is None else env)
+        e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nproc), LOCAL_WORLD_SIZE=str(nproc),
+                 MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, script, *argv], env=e))
+    codes = [p.wait() for p in procs]
+    bad = [c for c in codes if c != 0]
+    return bad[0] if bad else 0
+
+
+def cpu_info() -> dict:
+    """Host-core provenance for the CPU baselines (BASELINE.md plan)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = None
+    return {"nproc": os.cpu_count(), "affinity_cpus": aff, "cpu_model": model,
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
 
 
 def parse():
@@ -66,11 +120,14 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--channels", type=int, default=65536, help="channels per GPU (weak)")
+    ap.add_argument("--channels", type=int, default=65536,
+                    help="channels of the batch (split over the GPUs; per GPU with --weak)")
     ap.add_argument("--frames", type=int, default=32)
     ap.add_argument("--ebn0", type=float, default=1000.0, help=">= 100: noiseless")
     ap.add_argument("--seed", type=int, default=3)
-    ap.add_argument("--strong", action="store_true", help="split --channels across ranks")
+    ap.add_argument("--weak", action="store_true",
+                    help="every GPU demodulates its own --channels batch (default: C4's split)")
+    ap.add_argument("--strong", action="store_true", help="(the default) split --channels across GPUs")
     ap.add_argument("--mode", choices=tuple(MODES), default="reference",
                     help="receiver semantics: reference parity (default); dec752 "
                          "(decimated_frame[752]), fft (kiss_fft hunt) or both: SURVEY.md 8f "
@@ -225,41 +282,78 @@ def sweep(args):
                                                        for r in rows)}), flush=True)
 
 
+def valu_from_counters(nch: int, nf: int, mode: str, t_launch: float):
+    """VALU issue rate of rx_kernel + rx_data_kernel from MEASURED counters:
+    SQ_INSTS_VALU (wave-instructions, every pass summed over the chip) per
+    launch, from the rocprofv3 --pmc pass of this build committed under
+    profiles/ (pmc_valu.json, written by profiles/summarize.py), over the
+    kernel time measured live here.  Peak: one wave64 VALU instruction per
+    SIMD-32 per 2 cycles (MI355X_MICROARCH.md "Wave scheduling"), 1,024 SIMDs at
+    2.4 GHz = 1.229e12 wave-instr/s; packed fp32 (v_pk_*) measured at 3.47
+    cycles per wave-instruction per SIMD with two waves per SIMD
+    (profiles/calib/valu_rate_r01.txt), i.e. 0.708e12 wave-instr/s."""
+    path = os.path.join(ROOT, "profiles", "pmc_valu.json")
+    if not os.path.exists(path):
+        return None
+    p = json.load(open(path))
+    if p.get("channels") != nch or p.get("frames") != nf or p.get("mode", "reference") != mode:
+        return None
+    insts = p["valu_insts_per_launch"]
+    peak = VALU_SIMDS * VALU_CLOCK_GHZ * 1e9 / 2.0
+    peak_pk = VALU_SIMDS * VALU_CLOCK_GHZ * 1e9 / 3.47
+    ach = insts / t_launch
+    out = {"valu_insts_per_launch": insts, "achieved_winst_s": round(ach / 1e12, 4),
+           "peak_winst_s": round(peak / 1e12, 4), "frac": round(ach / peak, 4),
+           "packed_peak_winst_s": round(peak_pk / 1e12, 4), "frac_packed": round(ach / peak_pk, 4),
+           "unit": "1e12 wave64 VALU instructions/s", "source": p.get("source")}
+    if p.get("active_valu_frac") is not None:
+        out["sq_active_inst_valu_per_wave_cycle"] = p["active_valu_frac"]
+    if p.get("clock_ghz") is not None:
+        out["clock_ghz_under_profiler"] = p["clock_ghz"]
+    return out
+
+
 def main():
     args = parse()
     if args.sweep:
         return sweep(args)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # one process per GPU, started before this process touches HIP
+        sys.exit(launch(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank0 = int(os.environ.get("RANK", "0")) == 0
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    strong = not args.weak
     pool = None
-    if rank0 and world == 1 and args.cpu_all_channels > 0 and args.cpu_procs > 1:
+    if rank == 0 and args.cpu_all_channels > 0 and args.cpu_procs > 1:
         import multiprocessing as mp
         import oracle
         if oracle.ref_available(MODES[args.mode]):
             pool = mp.get_context("spawn").Pool(args.cpu_procs)   # before any GPU use
 
+    dist = None
+    if world > 1:
+        # host-side group: the timing barrier and the reductions only (the
+        # data path has no collective, SURVEY.md 8e)
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+
     import torch
     import singlecarrier_amd as sc
 
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-
-    nch, c0 = shard(args.channels, world, rank, args.strong)
+    nch, c0 = shard(args.channels, world, rank, strong)
     nf = args.frames
 
-    # input: generated on the GPU (qpsk_synth_device == the host generator,
+    # input: generated on the GPU (qpsk_synth_device == the oracle's generator,
     # tests/test_gpu_synth.py), resident in HBM before timing
     t = time.perf_counter()
     x = sc.synth_device(args.seed, nch, nf, args.ebn0, c0=c0, device=local)
     torch.cuda.synchronize()
     t_synth = time.perf_counter() - t
     # PCIe-inclusive reference point (never `value`), rank 0 only: the same
-    # batch copied in from pageable host memory
+    # batch copied in from pageable host memory.  Other ranks keep only the
+    # channels they verify.
     x_host, t_h2d = None, None
     if rank == 0:
         x_host = x.cpu().numpy()
@@ -268,6 +362,8 @@ def main():
         torch.cuda.synchronize()
         t_h2d = time.perf_counter() - t
         del x2
+    elif args.verify:
+        x_host = x[:min(args.verify, nch)].cpu().numpy()
     bits = torch.empty((nch, nf, 62), dtype=torch.uint8, device=x.device)
     valid = torch.empty((nch, nf), dtype=torch.uint8, device=x.device)
     mode = MODES[args.mode]
@@ -275,6 +371,7 @@ def main():
 
     for _ in range(args.warmup):
         rx.demod_device(x, bits, valid)
+    rx.sync()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -288,15 +385,16 @@ def main():
         rx.demod_device(x, bits, valid)
     ev1.record()
     torch.cuda.synchronize()
-    wall = time.perf_counter() - t0
     if dist:
         dist.barrier()
+    wall = time.perf_counter() - t0
+    rx.sync()   # a device-side failure of any timed call raises here
     rx_ms, data_ms, kern_frames = rx.collect_timing_split()
     kern_ms = rx_ms + data_ms
     rx.timing(False)
     region_ms = ev0.elapsed_time(ev1)
 
-    tmax, total_ch = reduce_step(dist, wall, nch, x.device)
+    tmax, total_ch = reduce_step(dist, wall, nch)
     samples = float(total_ch) * nf * FRAME * args.steps
     value = samples / tmax / 1e6
 
@@ -316,18 +414,15 @@ def main():
     pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc):
         p = json.load(open(pmc))
-        if p.get("channels") == nch and p.get("frames") == nf:
+        if p.get("channels") == nch and p.get("frames") == nf and p.get("mode", "reference") == args.mode:
             roofline["traffic"] = p["hbm_bytes_per_launch"]
             roofline["traffic_source"] = p.get("source")
-    per_gpu_sps = nch * nf * FRAME / t_launch
-    valu = {"ops_per_sample": OPS_PER_SAMPLE_MIN,
-            "achieved_Tops": round(per_gpu_sps * OPS_PER_SAMPLE_MIN / 1e12, 2),
-            "peak_Tops": VALU_PEAK_TOPS,
-            "frac": round(per_gpu_sps * OPS_PER_SAMPLE_MIN / 1e12 / VALU_PEAK_TOPS, 4)}
+    valu = valu_from_counters(nch, nf, args.mode, t_launch)
 
-    # parity spot check of the timed outputs (checker only; not timed)
+    # parity spot check of the timed outputs on every rank (checker only; not
+    # timed): the first k channels of the rank's shard
     verified = None
-    if args.verify and rank == 0:
+    if args.verify:
         import oracle
         k = min(args.verify, nch)
         # the timed context advanced (warmup + steps) batches of the same
@@ -336,8 +431,13 @@ def main():
         exp_bits, exp_valid, _ = oracle.cpu_rx(np.concatenate([x_host[:k]] * reps, axis=1),
                                                mode=mode)
         same_input = bool((oracle.synth(args.seed, k, nf, args.ebn0, c0=c0) == x_host[:k]).all())
-        verified = bool(same_input and (bits[:k].cpu().numpy() == exp_bits[:, -nf:]).all()
-                        and (valid[:k].cpu().numpy() == exp_valid[:, -nf:]).all())
+        ok = bool(same_input and (bits[:k].cpu().numpy() == exp_bits[:, -nf:]).all()
+                  and (valid[:k].cpu().numpy() == exp_valid[:, -nf:]).all())
+        verified = {"rank": rank, "channels": [c0, c0 + k], "ok": ok}
+    per_rank = [verified]
+    if dist:
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, verified)
 
     # streaming ingest (include/qpsk_stream.h): host chunks through pinned slots,
     # H2D / receive / D2H overlapped.  PCIe-inclusive; reported, never `value`.
@@ -365,32 +465,35 @@ def main():
                   "chunk": f"{nch} channels x {fpc} frames", "chunks": args.stream_chunks,
                   "slots": 3}
 
-    cpu = None
-    if rank == 0 and world == 1 and args.cpu_channels > 0:
+    # CPU baselines, rank 0, after the timed region (the other ranks wait at
+    # the final barrier): the C3 workload's channels 0.. regenerated on the host
+    cpu = cpu_all = None
+    host = cpu_info()
+    if rank == 0 and args.cpu_channels > 0:
         import oracle
         k = min(args.cpu_channels, nch)
-        sample = x_host[:k]
+        sample = x_host[:k] if c0 == 0 else oracle.synth(args.seed, k, nf, args.ebn0)
         if oracle.ref_available(mode):
             t = time.perf_counter()
             oracle.ref_rx(sample, mode=mode)
             dt = time.perf_counter() - t
             cpu = {"value": round(k * nf * FRAME / dt / 1e6, 3), "unit": "Msamples/s",
                    "cores": 1, "kind": "reference",
-                   "sample": f"{k} of the {nch} channels x {nf} frames, {_ref_name(mode)}, one channel "
-                             f"after another, {dt:.1f} s"}
+                   "sample": f"channels 0..{k - 1} of the {args.channels}-channel batch x {nf} "
+                             f"frames, {_ref_name(mode)}, one channel after another, {dt:.1f} s",
+                   **host}
         else:
             t = time.perf_counter()
             oracle.cpu_rx(sample, threads=1, mode=mode)
             dt = time.perf_counter() - t
             cpu = {"value": round(k * nf * FRAME / dt / 1e6, 3), "unit": "Msamples/s",
                    "cores": 1, "kind": "port",
-                   "sample": f"{k} channels x {nf} frames, oracle/cpu_ref.c, 1 thread, {dt:.1f} s"}
-
-    cpu_all = None
+                   "sample": f"{k} channels x {nf} frames, oracle/cpu_ref.c, 1 thread, {dt:.1f} s",
+                   **host}
     if pool is not None:
-        k = min(args.cpu_all_channels, nch)
+        k = min(args.cpu_all_channels, args.channels)
         bounds = np.linspace(0, k, args.cpu_procs + 1).astype(int)
-        jobs = [(args.seed, c0 + int(a), int(b - a), nf, args.ebn0, mode)
+        jobs = [(args.seed, int(a), int(b - a), nf, args.ebn0, mode)
                 for a, b in zip(bounds[:-1], bounds[1:]) if b > a]
         res = pool.map(_ref_timed, jobs)
         pool.close()
@@ -398,35 +501,44 @@ def main():
         tmx = max(r[1] for r in res)
         cpu_all = {"value": round(tot / tmx / 1e6, 3), "unit": "Msamples/s",
                    "cores": len(jobs), "kind": "reference",
-                   "sample": f"{k} of the {nch} channels x {nf} frames, {_ref_name(mode)}, "
-                             f"{len(jobs)} host processes, "
-                             f"slowest {tmx:.1f} s"}
+                   "sample": f"channels 0..{k - 1} of the {args.channels}-channel batch x {nf} "
+                             f"frames, {_ref_name(mode)}, {len(jobs)} host processes, "
+                             f"slowest {tmx:.1f} s", **host}
 
     if rank == 0:
+        ch_total = total_ch
         out = {
             "metric": METRIC, "value": round(value, 3), "unit": "Msamples/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(tmax / args.steps * 1e3, 3), "higher_is_better": True,
-            "scaling": "strong" if args.strong else "weak", "vs_baseline": None,
+            "scaling": "strong" if strong else "weak", "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic, generated on the GPU: reference TX packets, splitmix64 dibits, "
                     "per-channel delay"
                     + ("" if args.ebn0 >= 100 else f", AWGN Eb/N0 {args.ebn0} dB"),
-            "config": {"workload": f"{nch} channels x {nf} frames x 1880 samples per GPU "
-                                   f"(C3{'/C4' if world > 1 else ''})",
-                       "channels_per_gpu": nch, "channels_total": total_ch, "frames": nf,
-                       "samples_per_step": int(total_ch * nf * FRAME),
-                       "parallelism": f"channel shards x{world}, no collective",
+            "config": {"workload": (f"{ch_total} channels x {nf} frames x 1880 samples"
+                                    + (f", {world} channel shards of {nch}" if world > 1 and strong
+                                       else f" ({nch} per GPU)" if world > 1 else "")
+                                    + (" (C4)" if world > 1 and strong
+                                       else " (C3)" if ch_total == 65536 and nf == 32 else "")),
+                       "channels_per_gpu": nch, "channels_total": ch_total, "frames": nf,
+                       "samples_per_step": int(ch_total * nf * FRAME),
+                       "parallelism": f"{world} channel shard(s), one process per GPU, no "
+                                      f"collective (host gloo barrier/time reduction)",
                        "mode": args.mode},
             "roofline": roofline, "valu": valu, "cpu_baseline": cpu,
             "cpu_baseline_all_cores": cpu_all,
-            "region_ms_per_step": round(region_ms / args.steps, 3),
+            "rank0_region_ms_per_step": round(region_ms / args.steps, 3),
             "synth_s": round(t_synth, 2), "h2d_s": round(t_h2d, 2),
             "h2d_incl_msamples_s": round(nch * nf * FRAME / (t_h2d + tmax / args.steps) / 1e6, 1),
             "stream_pcie_note": "rank 0 only, after the timed region",
-            "verified_vs_oracle": verified, "stream_pcie": stream,
+            "verified_vs_oracle": all(v is not None and v["ok"] for v in per_rank) if args.verify else None,
+            "verified_per_rank": per_rank if args.verify else None,
+            "stream_pcie": stream,
         }
         print(json.dumps(out), flush=True)
+    if dist:
+        dist.barrier()
     rx.close()
     if dist:
         dist.destroy_process_group()

@@ -42,6 +42,12 @@ enum {
                              nch * nframes >= 2^28 in one call: 1 TB of input) */
     QPSK_ENOMEM = -2,     /* device or host allocation failed */
     QPSK_ENODEV = -3,     /* no such HIP device */
+    /* -4 is QPSK_EBUSY (qpsk_stream.h) */
+    QPSK_ESTALL = -5,     /* a device-side progress wait of rx_kernel's dual-chain
+                             shapes exceeded its bound (~0.1 s): the outputs of
+                             the calls since the previous check are undefined.
+                             Never expected; it turns a logic error into an
+                             error code instead of a hung GPU or wrong bits. */
     QPSK_EHIP = -1000,    /* QPSK_EHIP - hipError_t */
 };
 
@@ -80,7 +86,8 @@ int qpsk_rx_mode(const qpsk_ctx *ctx);
 uint64_t qpsk_rx_frames(const qpsk_ctx *ctx);
 
 /* Host-memory call: copies `in` to the device, demodulates nframes frames of
- * every channel, copies the results back and synchronises. */
+ * every channel, copies the results back and synchronises; returns
+ * qpsk_rx_sync()'s verdict. */
 int qpsk_rx_batch(qpsk_ctx *ctx, const int16_t *in, int nframes, uint8_t *bits,
                   uint8_t *valid, int32_t *trace, float *soft);
 
@@ -92,6 +99,11 @@ int qpsk_rx_batch(qpsk_ctx *ctx, const int16_t *in, int nframes, uint8_t *bits,
 int qpsk_rx_batch_device(qpsk_ctx *ctx, const int16_t *d_in, int nframes,
                          uint8_t *d_bits, uint8_t *d_valid, int32_t *d_trace,
                          float *d_soft, void *stream);
+
+/* Waits for the context's latest qpsk_rx_batch_device call (its stream) and
+ * returns QPSK_ESTALL if any call since the previous check reported a
+ * device-side failure (the device error word is sticky until read), else 0. */
+int qpsk_rx_sync(qpsk_ctx *ctx);
 
 /* Kernel-time accounting.  When enabled, every qpsk_rx_batch_device call
  * records HIP events on its stream before rx_kernel, between the two kernels

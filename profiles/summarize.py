@@ -1,8 +1,10 @@
 """Summarise a profiles/profile.sh run: per-kernel average duration and
 per-dispatch PMC averages for rx_kernel / rx_data_kernel, HBM traffic per
 launch with the gfx950 FETCH_SIZE correction (MI355X_MICROARCH.md 'HBM':
-FETCH_SIZE counts half the bytes of wide coalesced reads -> x2), writes
-profiles/<tag>_summary.md and profiles/pmc_traffic.json.
+FETCH_SIZE counts half the bytes of wide coalesced reads -> x2), the VALU
+instruction count per launch (SQ_INSTS_VALU) and the LDS bank-conflict share;
+writes profiles/<tag>_summary.md, profiles/pmc_traffic.json and
+profiles/pmc_valu.json (bench.py reads the last two when the workload matches).
 
     python profiles/summarize.py gpurun_out/prof_v1 TAG CHANNELS FRAMES [SKIP [COUNT]]
 
@@ -90,12 +92,32 @@ lines += ["", "## Derived (per step = one rx_kernel + one rx_data_kernel launch)
 if "SQ_WAVE_CYCLES" in c and "SQ_BUSY_CYCLES" in c:
     lines.append(f"- VALU instructions per wave-cycle: {c['SQ_INSTS_VALU'] / max(c['SQ_WAVE_CYCLES'], 1):.3f}; "
                  f"SQ_ACTIVE_INST_VALU/SQ_WAVE_CYCLES = {c['SQ_ACTIVE_INST_VALU'] / c['SQ_WAVE_CYCLES']:.3f}")
+clock = None
 if "GRBM_GUI_ACTIVE" in c:
-    lines.append(f"- effective clock ~ GRBM_GUI_ACTIVE/8/t = {c['GRBM_GUI_ACTIVE'] / 8 / t_ns:.2f} GHz")
+    clock = c['GRBM_GUI_ACTIVE'] / 8 / t_ns
+    lines.append(f"- effective clock ~ GRBM_GUI_ACTIVE/8/t = {clock:.2f} GHz")
+if "SQ_LDS_BANK_CONFLICT" in c and "SQ_ACTIVE_INST_LDS" in c:
+    lines.append(f"- LDS bank conflicts: SQ_LDS_BANK_CONFLICT / SQ_ACTIVE_INST_LDS = "
+                 f"{c['SQ_LDS_BANK_CONFLICT'] / max(c['SQ_ACTIVE_INST_LDS'], 1):.3f}"
+                 + (f"; / SQ_LDS_IDX_ACTIVE = {c['SQ_LDS_BANK_CONFLICT'] / max(c['SQ_LDS_IDX_ACTIVE'], 1):.3f}"
+                    if "SQ_LDS_IDX_ACTIVE" in c else ""))
+valu_insts = c.get("SQ_INSTS_VALU", 0) + cd.get("SQ_INSTS_VALU", 0)
+if valu_insts:
+    lines.append(f"- VALU wave-instructions per step (SQ_INSTS_VALU, both kernels): {valu_insts:.4g}; "
+                 f"issue rate {valu_insts / t_step:.4g} per ns vs peak 1,024 SIMDs / 2 cycles x 2.4 GHz "
+                 f"= 1228.8 per ns: {valu_insts / t_step / 1228.8:.3f}")
 open(os.path.join("profiles", f"{tag}_summary.md"), "w").write("\n".join(lines) + "\n")
 json.dump({"channels": nch, "frames": nfr, "hbm_bytes_per_launch": int(fetch_b + write_b),
            "kernels": [K, KD],
            "fetch_bytes": int(fetch_b), "write_bytes": int(write_b),
            "source": f"profiles/{tag}_summary.md (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes)"},
           open(os.path.join("profiles", "pmc_traffic.json"), "w"), indent=1)
+if valu_insts:
+    json.dump({"channels": nch, "frames": nfr, "kernels": [K, KD],
+               "valu_insts_per_launch": int(valu_insts),
+               "active_valu_frac": (round(c["SQ_ACTIVE_INST_VALU"] / c["SQ_WAVE_CYCLES"], 4)
+                                    if "SQ_ACTIVE_INST_VALU" in c and "SQ_WAVE_CYCLES" in c else None),
+               "clock_ghz": round(clock, 3) if clock else None,
+               "source": f"profiles/{tag}_summary.md (rocprofv3 --pmc SQ_INSTS_VALU pass)"},
+              open(os.path.join("profiles", "pmc_valu.json"), "w"), indent=1)
 print("\n".join(lines))

@@ -35,7 +35,12 @@ class _CF(C.Structure):
 
 
 class QpskError(RuntimeError):
-    pass
+    """A negative QPSK_E* code from the library (``.code``)."""
+    code = 0
+
+
+# error codes (include/qpsk_batch.h, qpsk_stream.h)
+QPSK_EINVAL, QPSK_ENOMEM, QPSK_ENODEV, QPSK_EBUSY, QPSK_ESTALL = -1, -2, -3, -4, -5
 
 
 def build(verbose: bool = False) -> str:
@@ -80,6 +85,7 @@ def lib():
         L.qpsk_tx_frame.argtypes = [vp, vp, i32, C.c_bool]
         L.qpsk_surface_error.restype = i32
         L.qpsk_rx_timing_enable.argtypes = [vp, i32]
+        L.qpsk_rx_sync.argtypes = [vp]
         L.qpsk_rx_timing_collect.argtypes = [vp, C.POINTER(C.c_float), C.POINTER(C.c_int)]
         L.qpsk_rx_timing_split.argtypes = [vp, C.POINTER(C.c_float), C.POINTER(C.c_float),
                                            C.POINTER(C.c_int)]
@@ -117,7 +123,7 @@ def lib():
 
 
 SYMBOLS = ["qpsk_rx_create", "qpsk_rx_create_mode", "qpsk_rx_mode", "qpsk_rx_destroy", "qpsk_rx_reset", "qpsk_rx_channels",
-           "qpsk_rx_frames", "qpsk_rx_batch", "qpsk_rx_batch_device", "qpsk_strerror",
+           "qpsk_rx_frames", "qpsk_rx_batch", "qpsk_rx_batch_device", "qpsk_rx_sync", "qpsk_strerror",
            "cnormf", "qpsk_mod", "qpsk_demod", "qpsk_rx_frame", "qpsk_tx_frame",
            "qpsk_rx_init", "qpsk_tx_init", "qpsk_surface_error", "qpsk_tx_state_init",
            "qpsk_tx_frame_state", "qpsk_synth_batch", "qpsk_rx_timing_enable",
@@ -130,7 +136,9 @@ SYMBOLS = ["qpsk_rx_create", "qpsk_rx_create_mode", "qpsk_rx_mode", "qpsk_rx_des
 
 def _check(rc: int) -> None:
     if rc != 0:
-        raise QpskError(f"qpsk error {rc}: {lib().qpsk_strerror(rc).decode()}")
+        e = QpskError(f"qpsk error {rc}: {lib().qpsk_strerror(rc).decode()}")
+        e.code = rc
+        raise e
 
 
 def _ptr(a) -> int | None:
@@ -210,6 +218,11 @@ class Receiver:
         _check(lib().qpsk_rx_batch(self._h, _ptr(x), nf, _ptr(out["bits"]), _ptr(out["valid"]),
                                    _ptr(out.get("trace")), _ptr(out.get("soft"))))
         return out
+
+    def sync(self) -> None:
+        """Wait for the latest demod_device call; raise QpskError (QPSK_ESTALL)
+        if any call since the previous check failed on the device."""
+        _check(lib().qpsk_rx_sync(self._h))
 
     def demod_device(self, x, bits, valid, trace=None, soft=None, stream=None) -> None:
         """Device tensors (torch, on this device): enqueue on ``stream``

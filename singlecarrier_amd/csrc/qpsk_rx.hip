@@ -97,7 +97,9 @@ struct RxArgs {
     unsigned g0;             // global index of the call's first frame
     size_t jcap;             // job queue capacity (plane stride of the jobs)
     int roles;               // bit 0: back, bit 1: front (3 in production); bits 4-5:
-                             // issue priority boost (0 none, 1 front, 2 back)
+                             // issue priority boost (0 none, 1 front, 2 back);
+                             // bits 8-15: front stagger; bits 16-19: front split
+    int* err;                // device error word (kErrStall)
 };
 
 // Diagnostic build only (-DQPSK_STAMPS): per-phase cycle sums of the front
@@ -134,30 +136,23 @@ __device__ __forceinline__ void wave_lds_sync() {
 // Dual-chain kernel (rx_kernel<.., DUAL = true>): per-frame progress counters
 // in LDS instead of a workgroup barrier.  Every wave of the (single) workgroup
 // is resident, and every counter is advanced by every frame of its producer,
-// so each wait ends; the bound only turns a logic error into wrong output
-// instead of a hung GPU.
-__device__ __forceinline__ void spin_wait(int* p, int v) {
-    for (unsigned it = 0; it < (1u << 22); it++) {   // ~0.1 s; a frame is ~2.5k spins
+// so each wait ends.  The bound keeps a logic error from hanging the GPU: a
+// wait that runs out sets kErrStall in the call's device error word, which
+// the host returns as QPSK_ESTALL (qpsk_rx_sync / qpsk_rx_batch), so stale
+// windows or rx_timing never pass as a result.
+constexpr unsigned kSpinBound = 1u << 22;   // ~0.1 s; a frame is ~2.5k spins
+constexpr int kErrStall = 1;                // device error word bits
+
+__device__ __forceinline__ void spin_wait(int* p, int v, int* err, unsigned bound = kSpinBound) {
+    unsigned it = 0;
+    for (; it < bound; it++) {
         const int c = __builtin_amdgcn_readfirstlane(
             __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
         if (c >= v) break;
         __builtin_amdgcn_s_sleep(1);
     }
+    if (it == bound && __lane_id() == 0) atomicOr(err, kErrStall);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
-
-// spin_wait that reports a timeout (the flow kernel's front waves stop waiting
-// after one, so a logic error costs 0.1 s per wave, not per channel)
-__device__ __forceinline__ bool spin_wait_b(int* p, int v) {
-    bool ok = false;
-    for (unsigned it = 0; it < (1u << 22); it++) {
-        const int c = __builtin_amdgcn_readfirstlane(
-            __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-        if (c >= v) { ok = true; break; }
-        __builtin_amdgcn_s_sleep(1);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    return ok;
 }
 
 // publish: every earlier store of this wave (LDS and global) is visible to the
@@ -729,6 +724,7 @@ __device__ __forceinline__ void load_x0(const float4* wp, f2 (&x)[5]) {
 }
 
 constexpr int kForceExact = 64;   // roles bit: take the exact-division path (tests)
+constexpr int kDebugStall = 128;  // roles bit: force one progress wait past its bound (tests)
 
 #ifndef QPSK_TRAIN_UNROLL
 #define QPSK_TRAIN_UNROLL 4   // steps per loop iteration (register reuse; A/B knob)
@@ -810,176 +806,6 @@ __device__ __forceinline__ void back_frame(const RxArgs& a, int ch, bool live, i
         a.valid[cf] = valid ? 1 : 0;
         if (a.trace)
             *reinterpret_cast<int4*>(a.trace + cf * 4) = make_int4(mi, matches, valid ? 1 : 0, rtn);
-    }
-}
-
-// ------------------------------------------------------------ flow back wave
-// rx_kernel<.., FLOW = true>: lane = channel, and every lane runs its own
-// frames.  The frame decision (src/qpsk.c:196: valid iff matches > 98) is
-// settled once 30 of the 128 training steps have missed; the rest of such a
-// frame's training is unobservable (an invalid frame outputs zeros and keeps
-// rx_timing), so the lane finishes it there and starts its next frame while
-// its neighbours are still training.  Per-channel LDS counters replace the
-// per-frame barrier: fdone[c] = fronts finished for channel c (window n and
-// mi_n ready when fdone >= n), bdone[c] = frames decided (rt_n ready when
-// bdone >= n).  The trace (tests) reports matches of all 128 steps, so a traced
-// call, or roles bit kNoEarly, trains every frame to the end.
-constexpr int kNoEarly = 1 << 20;     // roles bit (QPSK_EARLY=0)
-constexpr int kMissMax = QK_NPRE - QK_MATCH_MIN;   // 30 misses: matches <= 98, invalid
-
-// 4 x train_eq from slot i + 1 (i % 4 == 0, per lane); nib = preamble bits i..i+3
-template <bool EXACT>
-__device__ __forceinline__ void train4(Kal& k, f2 (&x)[5], const f2* wp2, int i, unsigned nib,
-                                       int& matches, bool& bad) {
-#pragma unroll
-    for (int t = 0; t < 4; t++) {
-        const f2 nx = wp2[i + t + 6];
-        const float ref = ((nib >> t) & 1u) ? 1.0f : -1.0f;
-        f2 v = {0.0f, 0.0f};
-#pragma unroll
-        for (int s = 0; s < 5; s++) v = v + cmul(x[s], k.eq[s]);
-        const float er = ref - v.x;
-        update_eq<EXACT>(k, x, f2{er, v.y}, bad);
-        if (er * ref > 0.0f) matches++;
-#pragma unroll
-        for (int s = 0; s < 4; s++) x[s] = x[s + 1];
-        x[4] = nx;
-    }
-}
-
-__device__ __forceinline__ int lds_load(const int* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-__device__ __forceinline__ f2 sel(bool c, f2 a, f2 b) { return f2{c ? a.x : b.x, c ? a.y : b.y}; }
-
-// the lane id, recomputed where used (volatile: not hoisted into a register that
-// lives across the training steps)
-__device__ __forceinline__ int lane_fresh() {
-    int l;
-    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
-    return l;
-}
-
-// One back wave of the flow kernel: group channels ch0 + lane (lane < nlive).
-// mi / rt: the group's mi_s / rt_s [parity][lane]; fdone / bdone per lane.
-// The training steps run on every lane of the wave under uniform control flow
-// (a lane without a frame computes on stale state and its results are never
-// used), so the equalizer state has one home in registers; lanes start a frame
-// by select, not by branch.  A lane whose fast-reciprocal operands left their
-// range (`bad`) trains the frame again with IEEE division; while one does, the
-// whole wave takes the exact step, which equals the fast one on in-range lanes.
-__device__ __forceinline__ void back_flow(const RxArgs& a, int ch0, int nlive, int (*mi)[QK_GROUP],
-                                          int (*rt)[QK_GROUP], int* fdone, int* bdone,
-                                          const unsigned char* nibs) {
-    const int lane = lane_id();
-    const int ch = ch0 + lane;
-    const bool early = a.trace == nullptr && (a.roles & kNoEarly) == 0;
-    const bool force = (a.roles & kForceExact) != 0;
-    int n = lane < nlive ? 0 : a.F;    // this lane's frame
-    bool act = false, bad = false, exact = false;
-    int i = 0, matches = 0;
-    Kal k = kal_reset();
-    // a lane without a frame reads the group's first window (always in bounds)
-    const f2* wp2 = reinterpret_cast<const f2*>(win_of(a, a.g0) + (size_t)ch0 * kWinStride);
-    f2 x[5];
-    load_x0(reinterpret_cast<const float4*>(wp2), x);
-    for (unsigned idle = 0; idle < (1u << 22);) {   // ~0.1 s with every lane waiting: a logic error
-        // idle lanes with a frame left start it once its window is there
-        const bool want = !act && n < a.F;
-        if (__ballot(want)) {
-            const bool go = want && lds_load(fdone + lane_fresh()) >= n;
-            if (__ballot(go)) {
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                int chl = ch;
-                asm volatile("" : "+v"(chl));   // no per-lane address hoisted out of the loop
-                const f2* nw = reinterpret_cast<const f2*>(win_of(a, a.g0 + (unsigned)min(n, a.F - 1)) +
-                                                           (size_t)chl * kWinStride);
-                wp2 = go ? nw : wp2;
-                const Kal r = kal_reset();
-#pragma unroll
-                for (int t = 0; t < 5; t++) {
-                    k.eq[t] = sel(go, r.eq[t], k.eq[t]);
-                    k.d[t] = sel(go, r.d[t], k.d[t]);
-                }
-#pragma unroll
-                for (int t = 0; t < 10; t++) k.u[t] = sel(go, r.u[t], k.u[t]);
-                f2 x0[5];
-                load_x0(reinterpret_cast<const float4*>(wp2), x0);
-#pragma unroll
-                for (int t = 0; t < 5; t++) x[t] = sel(go, x0[t], x[t]);
-                i = go ? 0 : i;
-                matches = go ? 0 : matches;
-                bad = go ? force && !exact : bad;
-                act = act || go;
-            }
-        }
-        if (__ballot(act) == 0ull) {
-            if (__ballot(n < a.F) == 0ull) break;
-            __builtin_amdgcn_s_sleep(1);
-            idle++;
-            continue;
-        }
-        idle = 0;
-        {
-            const unsigned nib = nibs[i >> 2];   // preamble bits i..i+3 (LDS)
-            if (__ballot(act && exact)) train4<true>(k, x, wp2, i, nib, matches, bad);
-            else train4<false>(k, x, wp2, i, nib, matches, bad);
-            i += act ? 4 : 0;   // a lane without a frame stays inside its window
-        }
-        const bool fin = act && (i == QK_NPRE || (early && i - matches >= kMissMax));
-        if (__ballot(fin) == 0ull) continue;
-        if (fin && bad && !exact) {   // train the frame again, exactly
-            exact = true;
-            act = false;
-        }
-        const bool done = fin && act;
-        if (__ballot(done) == 0ull) continue;
-        if (done) {
-            const int lane = lane_fresh();
-            const bool valid = matches > QK_MATCH_MIN;
-            int chl = ch;
-            asm volatile("" : "+v"(chl));   // no per-lane address hoisted out of the loop
-            const size_t cf = (size_t)chl * a.F + n;
-            // mi_n and rt_n stay in LDS during the training (register pressure);
-            // the front rewrites neither before this frame is decided
-            const int mi_n = mi[n & 1][lane];
-            int rt_n = rt[n & 1][lane];
-            const unsigned long long vm = __ballot(valid);   // finishing lanes only
-            if (vm) {
-                const int first = __builtin_ctzll(__ballot(1));
-                unsigned base = 0;
-                if (lane == first) base = atomicAdd(a.njobs, (unsigned)__popcll(vm));
-                base = __shfl(base, first);
-                if (valid) {
-                    const unsigned slot = base + __builtin_amdgcn_mbcnt_hi(
-                        (unsigned)(vm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)vm, 0u));
-                    DataJob j;
-                    j.k = k;
-                    j.cf = cf;
-                    j.ks = (a.g0 + (unsigned)n) % QK_KS_FRAMES;
-                    put_job(a.jobs, a.jcap, slot, j, wp2 + 129);
-                }
-            }
-            if (!valid) {   // invalid frame: bits (and soft symbols) are zero
-                uint16_t* bo = reinterpret_cast<uint16_t*>(a.bits + cf * QK_NBITS);
-                for (int ss = 0; ss < QK_NDSYM; ss++) bo[ss] = 0;
-                if (a.soft) {
-                    float2* so = a.soft + cf * QK_NDSYM;
-                    for (int ss = 0; ss < QK_NDSYM; ss++) so[ss] = make_float2(0.0f, 0.0f);
-                }
-            }
-            if (valid) rt_n = mi_n + QK_NPRE;   // src/qpsk.c:219
-            a.valid[cf] = valid ? 1 : 0;
-            if (a.trace)
-                *reinterpret_cast<int4*>(a.trace + cf * 4) = make_int4(mi_n, matches, valid ? 1 : 0, rt_n);
-            rt[(n + 1) & 1][lane] = rt_n;
-            n++;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            __hip_atomic_store(bdone + lane, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            act = false;
-            exact = false;
-        }
     }
 }
 
@@ -1067,7 +893,7 @@ __global__ void __launch_bounds__(256) rx_data_kernel(const float4* jobs, unsign
 // the argument block is indexed dynamically (no scratch copy).
 // 12 waves per workgroup, 3 per SIMD (<= 168 VGPRs), one workgroup per CU (LDS).
 //
-// DUAL (G == 1 only): two back waves, one for the even and one for the odd
+// DUAL (G <= 2): two back waves per group, one for the even and one for the odd
 // frames of the call.  Frame n's training needs only frame n-1's front, and
 // frame n-1's front needs frame n-2's decision, so consecutive frames' training
 // is independent: the back of frame n+1 starts as soon as the front of frame n
@@ -1080,15 +906,12 @@ __global__ void __launch_bounds__(256) rx_data_kernel(const float4* jobs, unsign
 // W (DUAL only): channels per group, 64, 32 or 16.  A narrower group leaves
 // back lanes idle but spreads a small batch over more CUs and gives each front
 // wave fewer channels per frame, which shortens the front half of the chain.
-//
-// FLOW (not DUAL): back_flow() backs with early-terminated training and
-// per-channel progress counters instead of the per-frame __syncthreads().
-template <int G, int FP, int MODE, bool DUAL, int W = QK_GROUP, bool FLOW = false>
+template <int G, int FP, int MODE, bool DUAL, int W = QK_GROUP>
 __global__ void __launch_bounds__(64 * G * ((DUAL ? 2 : 1) + FP), 3) rx_kernel(
     const int16_t* in, int16_t* hist, const float2* ptab, const unsigned long long* ks,
     float2* win0, float2* win1, int* mi0, int* mi1, int* rt0, int* rt1, uint8_t* bits,
     uint8_t* valid, int32_t* trace, float2* soft, float4* jobs, unsigned* njobs, int nch, int F,
-    unsigned g0, int roles, const float* fft_tab, unsigned long long jcap) {
+    unsigned g0, int roles, const float* fft_tab, unsigned long long jcap, int* err) {
     static_assert(W == QK_GROUP || (DUAL && G == 1 && W % FP == 0 && W <= QK_GROUP), "group width");
     constexpr int kGroups = G, kFrontPer = FP;
     constexpr int kBackWaves = DUAL ? 2 * kGroups : kGroups;
@@ -1096,7 +919,7 @@ __global__ void __launch_bounds__(64 * G * ((DUAL ? 2 : 1) + FP), 3) rx_kernel(
     constexpr int kFrontWaves = kGroups * kFrontPer;
     constexpr int kBlock = 64 * (kBackWaves + kFrontWaves);
     const RxArgs a{in, hist, ptab, ks, win0, win1, mi0, mi1, rt0, rt1, bits, valid, trace, soft,
-                   jobs, njobs, nch, F, g0, (size_t)jcap, roles};
+                   jobs, njobs, nch, F, g0, (size_t)jcap, roles, err};
     __shared__ __attribute__((aligned(16))) float2 P[QK_FRAME];
     constexpr int DM = MODE & 1;   // decimation semantics; MODE & 2: FFT hunt
     constexpr int kM = Cfg<DM>::kM, kDecBuf = Cfg<DM>::kDecBuf;
@@ -1106,8 +929,6 @@ __global__ void __launch_bounds__(64 * G * ((DUAL ? 2 : 1) + FP), 3) rx_kernel(
     // hunt tables: the MFMA correlator's B, or the FFT hunt's twiddles / Q / permutation
     __shared__ __attribute__((aligned(16))) float BT[(MODE & 2) ? kFftHT : qhunt::kBT];
     __shared__ int bseq[kGroups][2], fcnt[kGroups][2];   // DUAL progress counters, per group
-    __shared__ int fdone[FLOW ? kGroups : 1][QK_GROUP], bdone[FLOW ? kGroups : 1][QK_GROUP];   // FLOW
-    __shared__ unsigned char pre_nib[QK_NPRE / 4];   // FLOW: preamble bits 4i..4i+3
     const int lane = threadIdx.x & 63;
     // wave-uniform by construction; readfirstlane tells the compiler, so every
     // per-wave index and pointer below lives in SGPRs
@@ -1128,99 +949,7 @@ __global__ void __launch_bounds__(64 * G * ((DUAL ? 2 : 1) + FP), 3) rx_kernel(
         }
     }
     if (threadIdx.x < 2 * kGroups) (&bseq[0][0])[threadIdx.x] = (&fcnt[0][0])[threadIdx.x] = 0;
-    if constexpr (FLOW) {
-        for (int i = threadIdx.x; i < kGroups * QK_GROUP; i += kBlock)
-            (&fdone[0][0])[i] = (&bdone[0][0])[i] = 0;
-        if (threadIdx.x < QK_NPRE / 4)
-            pre_nib[threadIdx.x] = (unsigned char)(((threadIdx.x < 16 ? kPreLo : kPreHi) >> (4 * (threadIdx.x & 15))) & 15u);
-    }
     __syncthreads();
-    if constexpr (FLOW) {
-        static_assert(!DUAL, "flow kernel: one back wave per group");
-        if (wave < kGroups) {
-            const int gi = wave;
-            const int gch0 = (grp0 + gi) * QK_GROUP;
-            const int nl = max(0, min(QK_GROUP, a.nch - gch0));
-            if (((a.roles >> 4) & 3) == 2) __builtin_amdgcn_s_setprio(2);
-            if (nl > 0) back_flow(a, gch0, nl, mi_s[gi], rt_s[gi], fdone[gi], bdone[gi], pre_nib);
-        } else {
-            const int f = wave - kGroups;
-            const int gi = f / kFrontPer;
-            const int cbeg = (f % kFrontPer) * kFrontCh;
-            const int ch0 = (grp0 + gi) * QK_GROUP + cbeg;
-            const int nlive = max(0, min(kFrontCh, a.nch - ch0));
-            float2* M = Ms[f];
-            int pf[kPf<DM>];
-            if (((a.roles >> 4) & 3) == 1) __builtin_amdgcn_s_setprio(2);
-            if (nlive > 0) prefetch<DM>(srcs(a, ch0, 0), lane, pf);
-            // the younger front wave of each SIMD starts late once (QPSK_STAGGER)
-            for (int z = (f >= kFrontWaves / 2) ? (a.roles >> 8) & 255 : 0; z > 0; z--)
-                __builtin_amdgcn_s_sleep(8);
-            // windows stored and published to the back, in (frame, channel)
-            // order: npub windows published, the next is channel pc of frame pn.
-            // A window is published once a later vmcnt wait has covered its
-            // store (after the next channel's mix).
-            int nst = 0, npub = 0, pc = 0, pn = 0;
-            auto publish = [&] {
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                for (; npub < nst; npub++) {
-                    if (lane == 0)
-                        __hip_atomic_store(&fdone[gi][cbeg + pc], pn + 1, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_WORKGROUP);
-                    if (++pc == nlive) { pc = 0; pn++; }
-                }
-            };
-            bool dead = false;
-            for (int n = 0; n < a.F; n++) {
-                const int p = n & 1;
-                const unsigned g = a.g0 + (unsigned)n;
-                float2* wout = win_of(a, g + 1u);
-                int pmi = 0;
-                for (int c = 0; c < nlive; c++) {
-                    const int ch = ch0 + c;
-                    float2* dcur = decs[f][c % kDecBuf];
-                    mix<DM>(lane, pf, g, P, M);
-                    publish();
-                    if (c > 0) {
-                        store_window(lane, pmi, decs[f][(c - 1) % kDecBuf], wout + (size_t)(ch - 1) * kWinStride);
-                        nst++;
-                    }
-                    {
-                        const bool same = c + 1 < nlive;
-                        if (same || n + 1 < a.F)
-                            prefetch<DM>(srcs(a, same ? ch + 1 : ch0, same ? n : n + 1), lane, pf);
-                    }
-                    wave_lds_sync();
-                    // back(n-1) of this channel decided: rt_n, and window n+1's buffer
-                    // (window n-1) and mi_s[p ^ 1] (mi_{n-1}) are free
-                    if (n > 0 && !dead) dead = !spin_wait_b(&bdone[gi][cbeg + c], n);
-#ifdef QPSK_STAMPS
-                    unsigned long long st_acc[16];   // flow shapes are not stamped
-#endif
-                    pmi = front_channel<MODE>(lane, rt_s[gi][p][cbeg + c], M, dcur, BT FACC_ARG);
-                    if (lane == 0) mi_s[gi][p ^ 1][cbeg + c] = pmi;
-                    if (c + 1 == nlive) {
-                        store_window(lane, pmi, dcur, wout + (size_t)ch * kWinStride);
-                        nst++;
-                    }
-                    wave_lds_sync();
-                }
-            }
-            publish();
-            carry_history<DM>(a.in, a.hist, a.F, ch0, nlive, lane);
-        }
-        __syncthreads();
-        if (wave < kGroups) {   // state after the call's last frame
-            const int ch = (grp0 + wave) * QK_GROUP + lane;
-            if (ch < a.nch) {
-                const unsigned ge = a.g0 + (unsigned)a.F;
-                mi_of(a, ge)[ch] = mi_s[wave][a.F & 1][lane];
-                rt_of(a, ge)[ch] = rt_s[wave][a.F & 1][lane];
-            }
-        }
-        return;
-    }
     if constexpr (DUAL) {
         if (wave < kBackWaves) {
             // ---------------------------------------------------- back of group wave/2,
@@ -1229,13 +958,17 @@ __global__ void __launch_bounds__(64 * G * ((DUAL ? 2 : 1) + FP), 3) rx_kernel(
             const int ch = (grp0 + gi) * W + lane;
             const bool live = lane < W && ch < a.nch;
             if (((a.roles >> 4) & 3) == 2) __builtin_amdgcn_s_setprio(2);
+            // tests (roles bit kDebugStall): one wait that cannot end, on the
+            // first back wave of workgroup 0, with a short bound
+            if ((a.roles & kDebugStall) && blockIdx.x == 0 && wave == 0)
+                spin_wait(&fcnt[gi][0], 1 << 30, a.err, 1u << 12);
             for (int n = wave & 1; n < a.F; n += 2) {
                 const int p = n & 1;
                 // front(n-1) done by every front wave of the group: window n and mi_n
-                if (n > 0) spin_wait(&fcnt[gi][p ^ 1], kFrontPer * ((n - 1) / 2 + 1));
+                if (n > 0) spin_wait(&fcnt[gi][p ^ 1], kFrontPer * ((n - 1) / 2 + 1), a.err);
                 back_frame(a, live ? ch : 0, live, n, mi_s[gi][p][lane],
                            [&] {   // rx_timing of frame n = the decision of frame n-1
-                               if (n > 0) spin_wait(&bseq[gi][p ^ 1], n);
+                               if (n > 0) spin_wait(&bseq[gi][p ^ 1], n, a.err);
                                return rt_s[gi][p][lane];
                            },
                            win_of(a, a.g0 + (unsigned)n) + (size_t)(live ? ch : 0) * kWinStride,
@@ -1247,10 +980,10 @@ __global__ void __launch_bounds__(64 * G * ((DUAL ? 2 : 1) + FP), 3) rx_kernel(
             const int f = wave - kBackWaves;
             const int gi = f / kFrontPer;
             const int fl = f % kFrontPer;
-            // roles bits 16-19 (QPSK_SPLIT = s, one group per workgroup only):
-            // the front waves that share a SIMD with a back wave (waves 4, 5,
-            // 8, 9 when waves map to SIMDs by wave % 4) take s channels fewer,
-            // the others s more
+            // roles bits 16-19 (split s, one group per workgroup only; pick_shape
+            // sets 2 at W = 64): the front waves that share a SIMD with a back
+            // wave (waves 4, 5, 8, 9 when waves map to SIMDs by wave % 4) take s
+            // channels fewer, the others s more
             const int split = kGroups == 1 ? (a.roles >> 16) & 15 : 0;
             auto share = [&](int x) { return ((x + kBackWaves) & 3) < kBackWaves; };
             int cbeg = 0;
@@ -1268,7 +1001,7 @@ __global__ void __launch_bounds__(64 * G * ((DUAL ? 2 : 1) + FP), 3) rx_kernel(
                 float2* wout = win_of(a, g + 1u);
                 // back(n-1) done: rx_timing of frame n, and window n+1's buffer
                 // (window n-1) and mi_s[p ^ 1] (mi_{n-1}) are free
-                if (n > 0) spin_wait(&bseq[gi][p ^ 1], n);
+                if (n > 0) spin_wait(&bseq[gi][p ^ 1], n, a.err);
                 int pmi = 0;
                 for (int c = 0; c < nlive; c++) {
                     const int ch = ch0 + c;
@@ -1353,7 +1086,7 @@ __global__ void __launch_bounds__(64 * G * ((DUAL ? 2 : 1) + FP), 3) rx_kernel(
             const unsigned g = a.g0 + (unsigned)n;
             float2* wout = win_of(a, g + 1u);
             int pmi = 0;
-            // roles bits 8-15 (QPSK_STAGGER): the second half of the front waves
+            // roles bits 8-15 (stagger, kStagger): the second half of the front waves
             // (the younger partner on each SIMD) starts each frame that many x
             // 512 cycles late, so partners' FIR and MFMA/LDS phases interleave
             // (MI355X_MICROARCH.md "two waves per SIMD", item 9)
@@ -1396,6 +1129,18 @@ float bits2f(uint32_t u) {
 
 }  // namespace
 
+// rx_kernel instantiations (pick_shape below)
+struct Shape {
+    enum Kind { k4x2, k2x4d, k1x8d16, k1x8d32, k1x8d64 };
+    int kind;
+    int roles;
+};
+
+constexpr int kStagger = 12;   // front stagger, 512-cycle units (roles bits 8-15)
+// rx_data_kernel grid: persistent, 4 workgroups of 256 per CU (other geometries
+// measured within 2%, profiles/r01_data_ab.txt)
+constexpr int kDataGrid = 1024, kDataBlock = 256;
+
 struct qpsk_ctx {
     int device = 0, nch = 0, ngroup = 0;
     int mode = QPSK_MODE_REFERENCE;   // receiver semantics, fixed at creation
@@ -1427,19 +1172,15 @@ struct qpsk_ctx {
     int ev_frames[kEv] = {};
     int ev_n = 0;
     bool timing = false;
-    // roles + priority + front stagger (12 x 512 cycles: -0.7%, profiles/r01_stagger_ab.txt);
-    // QPSK_ABLATE / QPSK_PRIO / QPSK_STAGGER (profiling)
-    int roles = 3 | (1 << 4) | (12 << 8);
+    // roles + front issue priority + front stagger (12 x 512 cycles: -0.7%,
+    // profiles/r01_stagger_ab.txt); QPSK_ABLATE (profiling), QPSK_FORCE_EXACT /
+    // QPSK_DEBUG_STALL (tests)
+    int roles = 3 | (1 << 4) | (kStagger << 8);
     int ncu = 256;              // compute units of the device
-    int shape_groups = 0;       // 0: by batch size; QPSK_SHAPE (A/B experiments)
-    bool single_back = false;   // QPSK_SHAPE=1x8s: G = 1 without the dual-chain back
-    int width = 0;              // dual-chain group width; 0: by batch size; QPSK_WIDTH
-    bool dual_multi = false;    // QPSK_SHAPE=4x1d: dual-chain backs, 4 groups x 1 front (A/B);
-                                // a 4x2 dual shape would need <= 128 VGPRs and spills
-    bool single2 = false;       // QPSK_SHAPE=2x4: 2 groups without the dual-chain backs
-    bool flow = false;          // QPSK_SHAPE=4x2f / 2x4f: flow backs (early-terminated training)
-    bool tuned_split = false;   // QPSK_SPLIT / QPSK_PRIO given: no per-shape defaults
-    int data_grid = 1024, data_block = 256;   // rx_data_kernel launch (QPSK_DATA_GRID/BLOCK)
+    int shape = -1;             // Shape::Kind forced by QPSK_SHAPE (A/B runs); -1: by batch size
+    int width = 0;              // dual-chain group width forced by QPSK_WIDTH; 0: by batch size
+    int* d_err = nullptr;       // device error word (kErrStall), cleared by qpsk_rx_sync
+    hipStream_t last = nullptr; // stream of the latest qpsk_rx_batch_device call
     float pend_ms[2] = {0.0f, 0.0f};
     int pend_frames = 0;
 };
@@ -1486,6 +1227,7 @@ static int ctx_alloc(qpsk_ctx* c) {
     HCHECK(hipMalloc(&c->d_ks, sizeof(unsigned long long) * QK_KS_FRAMES));
     HCHECK(hipMalloc(&c->d_hist, sizeof(int16_t) * nslot(c) * 2 * QK_FRAME));
     HCHECK(hipMalloc(&c->d_njobs, sizeof(unsigned) * 2));
+    HCHECK(hipMalloc(&c->d_err, sizeof(int)));
     for (int p = 0; p < 2; p++) {
         HCHECK(hipMalloc(&c->d_win[p], sizeof(float2) * nslot(c) * kWinStride));
         HCHECK(hipMalloc(&c->d_mi[p], sizeof(int) * nslot(c)));
@@ -1500,6 +1242,7 @@ extern "C" int qpsk_rx_reset(qpsk_ctx* c) {
     const size_t ns = nslot(c);
     HCHECK(hipMemsetAsync(c->d_hist, 0, sizeof(int16_t) * ns * 2 * QK_FRAME, c->stream));
     HCHECK(hipMemsetAsync(c->d_njobs, 0, sizeof(unsigned) * 2, c->stream));
+    HCHECK(hipMemsetAsync(c->d_err, 0, sizeof(int), c->stream));
     for (int p = 0; p < 2; p++) {
         HCHECK(hipMemsetAsync(c->d_win[p], 0, sizeof(float2) * ns * kWinStride, c->stream));
         HCHECK(hipMemsetAsync(c->d_mi[p], 0, sizeof(int) * ns, c->stream));
@@ -1522,6 +1265,7 @@ static void ctx_free(qpsk_ctx* c) {
         for (int j = 0; j < 3; j++)
             if (c->ev[i][j]) (void)hipEventDestroy(c->ev[i][j]);
     (void)hipFree(c->d_ptab);
+    (void)hipFree(c->d_err);
     (void)hipFree(c->d_jobs);
     (void)hipFree(c->d_njobs);
     (void)hipFree(c->d_ks);
@@ -1595,36 +1339,15 @@ extern "C" qpsk_ctx* qpsk_rx_create_mode(int device, int nch, int mode, int* err
         if (!strcmp(ab, "front")) c->roles = (c->roles & ~3) | 2;
         else if (!strcmp(ab, "back")) c->roles = (c->roles & ~3) | 1;
     }
-    if (const char* pr = getenv("QPSK_PRIO")) {     // issue-priority experiments
-        c->tuned_split = true;
-        const int v = !strcmp(pr, "front") ? 1 : !strcmp(pr, "back") ? 2 : 0;
-        c->roles = (c->roles & ~(3 << 4)) | (v << 4);
-    }
     if (getenv("QPSK_FORCE_EXACT")) c->roles |= kForceExact;   // tests: exact-division path
-    if (const char* e = getenv("QPSK_EARLY"))                   // flow shapes: 0 = train 128 steps
-        if (!strcmp(e, "0")) c->roles |= kNoEarly;
-    if (const char* g = getenv("QPSK_DATA_GRID")) c->data_grid = atoi(g) > 0 ? atoi(g) : 1024;
-    if (const char* b = getenv("QPSK_DATA_BLOCK"))
-        c->data_block = (atoi(b) >= 64 && atoi(b) <= 256 && atoi(b) % 64 == 0) ? atoi(b) : 256;
-    if (const char* sp = getenv("QPSK_SPLIT")) {
-        c->roles |= (atoi(sp) & 15) << 16;
-        c->tuned_split = true;
-    }
-    if (const char* st = getenv("QPSK_STAGGER")) c->roles = (c->roles & ~(255 << 8)) | ((atoi(st) & 255) << 8);
+    if (getenv("QPSK_DEBUG_STALL")) c->roles |= kDebugStall;   // tests: the QPSK_ESTALL path
     if (const char* w = getenv("QPSK_WIDTH")) {
         const int v = atoi(w);
         c->width = (v == 16 || v == 32 || v == 64) ? v : 0;
     }
-    if (const char* sh = getenv("QPSK_SHAPE"))
-    {
-        c->shape_groups = !strcmp(sh, "1x8") || !strcmp(sh, "1x8s") || !strcmp(sh, "1x8f") ? 1
-                        : !strcmp(sh, "2x4") || !strcmp(sh, "2x4d") ? 2
-                        : !strcmp(sh, "2x4f") ? 2
-                        : !strcmp(sh, "4x2") || !strcmp(sh, "4x1d") || !strcmp(sh, "4x2f") ? 4 : 0;
-        c->dual_multi = !strcmp(sh, "4x1d");
-        c->flow = !strcmp(sh, "4x2f") || !strcmp(sh, "2x4f") || !strcmp(sh, "1x8f");
-        c->single2 = !strcmp(sh, "2x4");
-        c->single_back = !strcmp(sh, "1x8s");
+    if (const char* sh = getenv("QPSK_SHAPE")) {
+        c->shape = !strcmp(sh, "4x2") ? Shape::k4x2 : !strcmp(sh, "2x4d") ? Shape::k2x4d
+                 : !strcmp(sh, "1x8") ? Shape::k1x8d64 : -1;
     }
     int r = herr(hipSetDevice(device));
     if (r == QPSK_OK) {
@@ -1674,39 +1397,23 @@ extern "C" uint64_t qpsk_rx_frames(const qpsk_ctx* c) { return c ? c->frames : 0
 //     channels) that still fits the batch in one wave of workgroups; at
 //     W = 64 with back priority and 2 channels moved off each front wave that
 //     shares a SIMD with a back wave (-3%, profiles/r01_split_ab.txt).
-// QPSK_SHAPE (4x2 | 4x1d | 2x4 | 2x4d | 1x8 | 1x8s | 4x2f | 2x4f | 1x8f), QPSK_WIDTH,
-// QPSK_SPLIT and QPSK_PRIO override for A/B runs.  The flow shapes (f) are
-// exact but slower (DESIGN.md "Next" item 2, profiles/r01_flow_ab.txt).
-struct Shape {
-    enum Kind { k4x2, k4x1d, k2x4, k2x4d, k1x8, k1x8d16, k1x8d32, k1x8d64, k4x2f, k2x4f, k1x8f } kind;
-    int roles;
-};
-
+// QPSK_SHAPE (4x2 | 2x4d | 1x8) and QPSK_WIDTH force a shape for tests and A/B
+// runs.  Measured and dropped (records in profiles/): 4x1d, 2x4 and 1x8 with
+// single back waves, the early-terminated flow kernel (r01_flow_ab.txt).
 static Shape pick_shape(const qpsk_ctx* c) {
-    const int G = c->shape_groups > 0 ? c->shape_groups
-                : c->ngroup <= c->ncu ? 1 : c->ngroup <= 2 * c->ncu ? 2 : 4;
-    Shape sh{Shape::k4x2, c->roles};
-    if (G == 4) {
-        sh.kind = c->dual_multi ? Shape::k4x1d : c->flow ? Shape::k4x2f : Shape::k4x2;
-    } else if (G == 2) {
-        sh.kind = c->single2 ? Shape::k2x4 : c->flow ? Shape::k2x4f : Shape::k2x4d;
-    } else if (c->single_back) {
-        sh.kind = Shape::k1x8;
-    } else if (c->flow) {
-        sh.kind = Shape::k1x8f;
-    } else {
+    Shape sh{c->shape, c->roles};
+    if (sh.kind < 0)
+        sh.kind = c->ngroup <= c->ncu ? Shape::k1x8d64 : c->ngroup <= 2 * c->ncu ? Shape::k2x4d
+                                                                                  : Shape::k4x2;
+    if (sh.kind == Shape::k1x8d64) {
         const int W = c->width > 0 ? c->width
                     : (size_t)c->nch <= (size_t)16 * c->ncu ? 16
                     : (size_t)c->nch <= (size_t)32 * c->ncu ? 32 : 64;
         sh.kind = W == 16 ? Shape::k1x8d16 : W == 32 ? Shape::k1x8d32 : Shape::k1x8d64;
-        if (W == 64 && !c->tuned_split)
-            sh.roles = (sh.roles & ~((3 << 4) | (15 << 16))) | (2 << 4) | (2 << 16);
+        if (W == 64) sh.roles = (sh.roles & ~((3 << 4) | (15 << 16))) | (2 << 4) | (2 << 16);
     }
     return sh;
 }
-
-// rx_data_kernel grid: persistent, 4 workgroups of 256 per CU (qpsk_ctx::data_grid/block;
-// other geometries measured within 2%, profiles/r01_data_ab.txt)
 
 extern "C" int qpsk_rx_batch_device(qpsk_ctx* c, const int16_t* d_in, int F, uint8_t* d_bits,
                                     uint8_t* d_valid, int32_t* d_trace, float* d_soft,
@@ -1747,29 +1454,23 @@ extern "C" int qpsk_rx_batch_device(qpsk_ctx* c, const int16_t* d_in, int F, uin
     }
     const int parity = (int)(c->calls & 1u);
     const Shape sh = pick_shape(c);
-#define QPSK_LAUNCH(GG, FF, MM, DD, WW, FL)                                                    \
-    hipLaunchKernelGGL((rx_kernel<GG, FF, MM, DD, WW, FL>),                                    \
+#define QPSK_LAUNCH(GG, FF, MM, DD, WW)                                                        \
+    hipLaunchKernelGGL((rx_kernel<GG, FF, MM, DD, WW>),                                        \
                        dim3((unsigned)((c->nch + (size_t)GG * WW - 1) / ((size_t)GG * WW))),   \
                        dim3(64 * GG * ((DD ? 2 : 1) + FF)), 0, s, d_in, c->d_hist, c->d_ptab,  \
                        c->d_ks, c->d_win[0], c->d_win[1], c->d_mi[0], c->d_mi[1], c->d_rt[0],  \
                        c->d_rt[1], d_bits, d_valid, d_trace, reinterpret_cast<float2*>(d_soft), \
                        c->d_jobs, c->d_njobs + parity, c->nch, F,                               \
                        (unsigned)(c->frames & 0xffffffffu), sh.roles, c->d_fft,                \
-                       (unsigned long long)c->jobs_cap)
+                       (unsigned long long)c->jobs_cap, c->d_err)
 #define QPSK_LAUNCH_MODE(MM)                                                                   \
     do {                                                                                       \
         switch (sh.kind) {                                                                     \
-            case Shape::k4x1d: QPSK_LAUNCH(4, 1, MM, true, 64, false); break;                  \
-            case Shape::k2x4d: QPSK_LAUNCH(2, 4, MM, true, 64, false); break;                  \
-            case Shape::k1x8d16: QPSK_LAUNCH(1, 8, MM, true, 16, false); break;                \
-            case Shape::k1x8d32: QPSK_LAUNCH(1, 8, MM, true, 32, false); break;                \
-            case Shape::k1x8d64: QPSK_LAUNCH(1, 8, MM, true, 64, false); break;                \
-            case Shape::k1x8: QPSK_LAUNCH(1, 8, MM, false, 64, false); break;                  \
-            case Shape::k2x4: QPSK_LAUNCH(2, 4, MM, false, 64, false); break;                  \
-            case Shape::k4x2f: QPSK_LAUNCH(4, 2, MM, false, 64, true); break;                  \
-            case Shape::k2x4f: QPSK_LAUNCH(2, 4, MM, false, 64, true); break;                  \
-            case Shape::k1x8f: QPSK_LAUNCH(1, 8, MM, false, 64, true); break;                  \
-            default: QPSK_LAUNCH(4, 2, MM, false, 64, false); break;                           \
+            case Shape::k2x4d: QPSK_LAUNCH(2, 4, MM, true, 64); break;                         \
+            case Shape::k1x8d16: QPSK_LAUNCH(1, 8, MM, true, 16); break;                       \
+            case Shape::k1x8d32: QPSK_LAUNCH(1, 8, MM, true, 32); break;                       \
+            case Shape::k1x8d64: QPSK_LAUNCH(1, 8, MM, true, 64); break;                       \
+            default: QPSK_LAUNCH(4, 2, MM, false, 64); break;                                  \
         }                                                                                      \
     } while (0)
     switch (c->mode) {
@@ -1782,14 +1483,29 @@ extern "C" int qpsk_rx_batch_device(qpsk_ctx* c, const int16_t* d_in, int F, uin
 #undef QPSK_LAUNCH
     HCHECK(hipGetLastError());
     if (slot >= 0) HCHECK(hipEventRecord(c->ev[slot][1], s));
-    hipLaunchKernelGGL(rx_data_kernel, dim3(c->data_grid), dim3(c->data_block), 0, s, c->d_jobs,
+    hipLaunchKernelGGL(rx_data_kernel, dim3(kDataGrid), dim3(kDataBlock), 0, s, c->d_jobs,
                        (unsigned long long)c->jobs_cap, c->d_njobs, c->d_ks, d_bits,
                        reinterpret_cast<float2*>(d_soft), parity, c->roles & kForceExact);
     HCHECK(hipGetLastError());
     if (slot >= 0) HCHECK(hipEventRecord(c->ev[slot][2], s));
     c->frames += (uint64_t)F;
     c->calls++;
+    c->last = s;
     return QPSK_OK;
+}
+
+// Waits for the context's latest call and reports a device-side failure of any
+// call since the previous check (the error word is sticky until read).
+extern "C" int qpsk_rx_sync(qpsk_ctx* c) {
+    if (!c) return QPSK_EINVAL;
+    HCHECK(hipSetDevice(c->device));
+    HCHECK(hipStreamSynchronize(c->last));
+    HCHECK(hipStreamSynchronize(c->stream));
+    int e = 0;
+    HCHECK(hipMemcpy(&e, c->d_err, sizeof e, hipMemcpyDeviceToHost));
+    if (e == 0) return QPSK_OK;
+    HCHECK(hipMemset(c->d_err, 0, sizeof(int)));
+    return QPSK_ESTALL;
 }
 
 extern "C" int qpsk_rx_timing_enable(qpsk_ctx* c, int on) {
@@ -1869,8 +1585,7 @@ extern "C" int qpsk_rx_batch(qpsk_ctx* c, const int16_t* in, int F, uint8_t* bit
     if (soft)
         HCHECK(hipMemcpyAsync(soft, c->s_soft, sizeof(float) * cf * QK_NDSYM * 2,
                               hipMemcpyDeviceToHost, c->stream));
-    HCHECK(hipStreamSynchronize(c->stream));
-    return QPSK_OK;
+    return qpsk_rx_sync(c);
 }
 
 #ifdef QPSK_STAMPS
@@ -1892,6 +1607,7 @@ extern "C" const char* qpsk_strerror(int err) {
         case QPSK_ENOMEM: return "out of memory";
         case QPSK_ENODEV: return "no such HIP device";
         case -4: return "every stream slot is in flight (retrieve first)";
+        case QPSK_ESTALL: return "a device-side progress wait exceeded its bound; the call's outputs are undefined";
         default: break;
     }
     if (err <= QPSK_EHIP) return hipGetErrorString((hipError_t)(QPSK_EHIP - err));

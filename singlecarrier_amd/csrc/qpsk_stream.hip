@@ -182,14 +182,4 @@ extern "C" int qpsk_stream_retrieve(qpsk_stream* s, const uint8_t** bits, const 
 
 extern "C" qpsk_ctx* qpsk_stream_ctx(qpsk_stream* s) { return s ? s->rx : nullptr; }
 
-extern "C" size_t qpsk_records(const uint8_t* bits, const uint8_t* valid, int nframes,
-                               uint8_t* out) {
-    size_t n = 0;
-    for (int f = 0; f < nframes; f++) {
-        if (!valid[f]) continue;
-        memcpy(out + n, bits + (size_t)f * QK_NBITS, QK_NBITS);             // src/qpsk.c:455
-        memset(out + n + QK_NBITS, 0, 496 - QK_NBITS);
-        n += 496;
-    }
-    return n;
-}
+// qpsk_records(): host C, qpsk_records.c

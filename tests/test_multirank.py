@@ -1,62 +1,86 @@
 """Multi-GPU path on CPU: world_size-2 gloo ranks exercise the bench's channel
-sharding (distinct channels per rank, no data-path collective) and its timing
-reduction (MAX over ranks of the timed region, SUM of channels)."""
+sharding (C4: one 65,536-channel batch split into contiguous channel shards,
+no data-path collective), its launcher (`bench.py --gpus N` without torchrun
+spawns one process per GPU) and its timing reduction (MAX over ranks of the
+timed region, SUM of channels) over the host gloo group."""
+import json
 import os
-import socket
+import subprocess
+import sys
+import textwrap
 
 import pytest
-import torch.multiprocessing as mp
 
 import bench
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
-def test_shard_weak_and_strong():
-    assert [bench.shard(65536, 8, r, False) for r in (0, 7)] == [(65536, 0), (65536, 7 * 65536)]
+
+def test_shard_strong_is_c4_split():
+    # C4: shard g = channels [g*C/N, (g+1)*C/N)
+    for n in (1, 2, 4, 8):
+        parts = [bench.shard(65536, n, r) for r in range(n)]
+        assert parts == [(65536 // n, r * 65536 // n) for r in range(n)]
     parts = [bench.shard(65536, 3, r, True) for r in range(3)]
     assert sum(n for n, _ in parts) == 65536
     assert [c0 for _, c0 in parts] == [0, parts[0][0], parts[0][0] + parts[1][0]]
     assert bench.shard(10, 4, 3, True) == (2, 8)
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+def test_shard_weak():
+    assert [bench.shard(65536, 8, r, False) for r in (0, 7)] == [(65536, 0), (65536, 7 * 65536)]
 
 
-def _worker(rank, world, port, q):
-    import torch
+WORKER = textwrap.dedent('''
+    import json, os, sys
+    sys.path.insert(0, {root!r})
     import torch.distributed as dist
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    nch, c0 = bench.shard(1000, world, rank, strong=True)
-    # synthetic per-rank inputs are distinct channel ids: same generator, offset c0
+    import bench
     import singlecarrier_amd as sc
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    assert os.environ["MASTER_ADDR"] == "127.0.0.1" and int(os.environ["LOCAL_RANK"]) == rank
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    nch, c0 = bench.shard(1000, world, rank)
+    # a rank's synthetic shard = the same channels of the whole batch (c0 offset)
     x = sc.synth(5, nch, 2, c0=c0)
-    tmax, total = bench.reduce_step(dist, 0.5 + rank, nch, torch.device("cpu"))
-    q.put((rank, nch, c0, tmax, total, int(x[0, 0, :100].astype("int64").sum())))
+    tmax, total = bench.reduce_step(dist, 0.5 + rank, nch)
+    rows = [None] * world
+    dist.all_gather_object(rows, {{"rank": rank, "ok": True}})
+    with open(os.path.join({out!r}, f"r{{rank}}.json"), "w") as f:
+        json.dump([rank, nch, c0, tmax, total, int(x[0, 0, :100].astype("int64").sum()), rows], f)
     dist.barrier()
     dist.destroy_process_group()
+''')
 
 
-def test_two_rank_gloo_sharding_and_reduction():
-    if not os.path.exists(os.path.join(os.path.dirname(bench.__file__), "singlecarrier_amd",
-                                       "libqpsk_hip.so")):
+def test_launcher_two_rank_gloo_sharding_and_reduction(tmp_path):
+    """bench.launch() is what `python bench.py --gpus 2` runs without torchrun:
+    two child processes with RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set, gloo on
+    127.0.0.1, MAX of times and SUM of channels on every rank."""
+    if not os.path.exists(os.path.join(ROOT, "singlecarrier_amd", "libqpsk_hip.so")):
         pytest.skip("library not built")
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
-    for p in procs:
-        p.start()
-    res = sorted(q.get(timeout=120) for _ in procs)
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
-    (r0, n0, c00, t0, tot0, s0), (r1, n1, c01, t1, tot1, s1) = res
+    script = tmp_path / "worker.py"
+    script.write_text(WORKER.format(root=ROOT, out=str(tmp_path)))
+    assert bench.launch(2, [], script=str(script)) == 0
+    res = [json.load(open(tmp_path / f"r{r}.json")) for r in range(2)]
+    (r0, n0, c00, t0, tot0, s0, g0), (r1, n1, c01, t1, tot1, s1, g1) = res
     assert (n0, n1, c00, c01) == (500, 500, 0, 500)
     assert t0 == t1 == 1.5 and tot0 == tot1 == 1000      # MAX of times, SUM of channels
+    assert g0 == g1 == [{"rank": 0, "ok": True}, {"rank": 1, "ok": True}]
     import singlecarrier_amd as sc
     assert s1 == int(sc.synth(5, 1, 2, c0=500)[0, 0, :100].astype("int64").sum())
+
+
+def test_launcher_reports_a_failing_rank(tmp_path):
+    script = tmp_path / "fail.py"
+    script.write_text("import os, sys\nsys.exit(3 if os.environ['RANK'] == '1' else 0)\n")
+    assert bench.launch(2, [], script=str(script)) == 3
+
+
+def test_bench_gpus_flag_spawns_ranks(tmp_path):
+    """`bench.py --gpus 2` with no WORLD_SIZE re-runs itself as 2 ranks (here
+    only up to the parser: --help exits before any GPU work)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--help"],
+                       env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "--weak" in r.stdout
