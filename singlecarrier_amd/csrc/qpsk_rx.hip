@@ -157,12 +157,6 @@ __device__ __forceinline__ void spin_wait(int* p, int v, int* err, unsigned boun
 
 // publish: every earlier store of this wave (LDS and global) is visible to the
 // workgroup before the counter moves
-__device__ __forceinline__ void signal_set(int* p, int v, int lane) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
 __device__ __forceinline__ void signal_add(int* p, int v, int lane) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -809,6 +803,256 @@ __device__ __forceinline__ void back_frame(const RxArgs& a, int ch, bool live, i
     }
 }
 
+// ---------------------------------------------------------------- quad back
+// Small batches (the dual-chain kernel at <= 32 channels per workgroup) are
+// bound by the latency of one channel's 128 serial train_eq steps, and a lane
+// per channel issues every one of the step's ~234 instructions: one wave
+// cannot issue faster than one VALU instruction per ~4.7 cycles
+// (profiles/calib/valu_rate_r01.txt), so a step costs ~1,100 cycles however
+// idle the SIMD is.  Here a QUAD of lanes owns a channel and splits the step:
+// lane c (0..3) of the quad holds
+//   row c of u          R[d-1] = u[c][c+d]        (0 past column 4)
+//   column c+1 of u     C[d-1] = u[c+1-d][c+1]    (0 above row 0; C[0] is R[0])
+//   d[c+1], eq[c] and (lane 3) eq[4]; d[0] is kept by all four lanes,
+// computes column c+1's f/g/s/y/d/h, row c's chain of 6.15/6.16 updates and the
+// 5-term sums by quad DPP (v_*_dpp quad_perm), ~135 instructions per step.
+// Every fp32 operation is the one update_eq() issues, on the same operands and
+// in the same order: the prefix sums (a[j], val) run sequentially over the
+// quad's lanes, zero padding enters only as (+-0) addends / factors of a
+// finite value, which leave every nonzero sum unchanged (the row chains are
+// independent across rows: row i uses only its own running g[i] and the
+// ORIGINAL g[j], h[j] of the columns right of it, src/kalman.c:131-139).
+namespace qd {
+constexpr int kB0 = 0x00, kB1 = 0x55, kB2 = 0xAA, kB3 = 0xFF;   // broadcast lane k of the quad
+constexpr int kRot1 = 0x93;   // [3,0,1,2]: lane c <- lane c-1 (lane 0 <- lane 3)
+constexpr int kRot2 = 0x4E;   // [2,3,0,1]: lane c <- lane c-2
+constexpr int kRot3 = 0x39;   // [1,2,3,0]: lane c <- lane c+1
+}
+
+template <int CTRL>
+__device__ __forceinline__ float qdf(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, true));
+}
+template <int CTRL>
+__device__ __forceinline__ f2 qd2(f2 v) { return f2{qdf<CTRL>(v.x), qdf<CTRL>(v.y)}; }
+
+struct QKal {
+    f2 R[4];      // R[d-1] = u[c][c+d]
+    f2 C[3];      // C[d-2] = u[c+1-d][c+1], d = 2..4
+    f2 eqr;       // eq_coeff[c]
+    f2 eq4;       // eq_coeff[4] (lane 3)
+    float d0;     // d[0]
+    float dc;     // d[c+1]
+};
+
+__device__ __forceinline__ QKal qkal_reset() {   // kalman_reset, src/kalman.c:42-55
+    QKal k;
+#pragma unroll
+    for (int i = 0; i < 4; i++) k.R[i] = f2{0.0f, 0.0f};
+#pragma unroll
+    for (int i = 0; i < 3; i++) k.C[i] = f2{0.0f, 0.0f};
+    k.eqr = k.eq4 = f2{0.0f, 0.0f};
+    k.d0 = k.dc = 1.0f;
+    return k;
+}
+
+// one train_eq step (src/equalizer.c:45-58 with update_eq/kalman_calculate,
+// exactly update_eq<EXACT>'s operations) on the quad layout.  X[d] = x[c+1-d]
+// (x[index+t] of the reference), zero before x[0].  Returns er = Re(error).
+template <bool EXACT>
+__device__ __forceinline__ float qstep(QKal& k, const f2 (&X)[5], float ref, int c, bool& bad) {
+    const float E = QK_KAL_E, q = QK_KAL_Q;
+    // 1 where row c has column c+d (d = 2, 3, 4), else 0: h of a missing
+    // column is multiplied by 0, so the padding entries of R stay +0
+    const float m2 = c < 3 ? 1.0f : 0.0f, m3 = c < 2 ? 1.0f : 0.0f, m4 = c < 1 ? 1.0f : 0.0f;
+    // val = sum_t x[t] * eq[t], t = 0..4 in order (src/equalizer.c:49-51)
+    const f2 p = cmul(X[1], k.eqr);       // lane c: x[c] * eq[c]
+    const f2 p4 = cmul(X[0], k.eq4);      // lane 3: x[4] * eq[4]
+    // (the empty asm keeps the two components scalar adds, so each folds its
+    // DPP source into one v_add_f32_dpp instead of two moves and a packed add)
+    float vr = 0.0f, vi = 0.0f;
+#define QV(CT, P)                                                   \
+    vr = vr + qdf<CT>(P.x); vi = vi + qdf<CT>(P.y);                 \
+    asm("" : "+v"(vr), "+v"(vi))
+    QV(qd::kB0, p); QV(qd::kB1, p); QV(qd::kB2, p); QV(qd::kB3, p); QV(qd::kB3, p4);
+#undef QV
+    const float er = ref - vr;            // conjf(ref - val) = (ref - vr, vi)
+    // column 0 (every lane): f0 = conj(x0), 6.2
+    const f2 x0 = qd2<qd::kB0>(X[1]);
+    const f2 f0 = conj2(x0);
+    const f2 g0 = f0 * k.d0;                              // 6.4
+    const f2 t0 = g0 * f0;
+    const float a0 = E + (t0.x + t0.y);                   // 6.5
+    // column c+1: f = u[0][j]*conj(x0) + conj(xj) + sum_{0<i<j} u[i][j]*conj(xi)
+    f2 f = addc(cmulc(k.C[2], X[4]), X[0]);
+    f = f + cmulc(k.C[1], X[3]);
+    f = f + cmulc(k.C[0], X[2]);
+    f = f + cmulc(k.R[0], X[1]);
+    const f2 g = f * k.dc;                                // 6.4
+    const f2 t = g * f;
+    const float s = t.x + t.y;
+    // 6.6 a[j] = a[j-1] + Re(g conj f), the quad's s in column order
+    const float a1 = a0 + qdf<qd::kB0>(s);
+    const float a2 = a1 + qdf<qd::kB1>(s);
+    const float a3 = a2 + qdf<qd::kB2>(s);
+    const float a4 = a3 + qdf<qd::kB3>(s);
+    const float hq = 1.0f + q;                            // 6.7
+    const float ht = a4 * q;
+    const float ap = c == 0 ? a0 : c == 1 ? a1 : c == 2 ? a2 : a3;   // a[c]
+    const float ao = ap + s;                              // a[c+1], the chain's own add
+    const float xs0 = a0 + ht, xso = ao + ht;
+    float y0, yo;
+    if (EXACT) {
+        y0 = qk_div_ieee(xs0);
+        yo = qk_div_ieee(xso);
+    } else {
+        bad |= !qk_rcp_in_range(xs0, xso);   // xs is nondecreasing in j (update_eq)
+        y0 = qk_rcp_fast(xs0);
+        yo = qk_rcp_fast(xso);
+    }
+    k.d0 = k.d0 * ((hq * (E + ht)) * y0);                 // 6.20
+    k.dc = k.dc * ((hq * (ap + ht)) * yo);                // 6.21, 6.13
+    // (every DPP move is made unconditionally, then selected: a move inside
+    // a conditional would become a branch, the intrinsic being convergent)
+    const float yr = qdf<qd::kRot1>(yo);
+    const float yp = c == 0 ? y0 : yr;                    // y[c]
+    const f2 h = (-f) * yp;                               // 6.11 h[c+1]
+    // row c (6.15/6.16) from g[c]: column c's gain (lane c-1; column 0: g0)
+    const f2 gr = qd2<qd::kRot1>(g);
+    f2 G = c == 0 ? g0 : gr;
+    {   // column c+1: this lane
+        const f2 B1 = k.R[0];
+        k.R[0] = B1 + cmulc(h, G);
+        G = G + cmulc(g, B1);
+    }
+    {   // column c+2 (lane c+1); none for row 3
+        const f2 hr = qd2<qd::kRot3>(h);
+        const f2 hd = hr * m2;
+        const f2 gd = qd2<qd::kRot3>(g);
+        const f2 B1 = k.R[1];
+        k.R[1] = B1 + cmulc(hd, G);
+        G = G + cmulc(gd, B1);
+    }
+    {   // column c+3 (lane c+2); none for rows 2, 3
+        const f2 hr = qd2<qd::kRot2>(h);
+        const f2 hd = hr * m3;
+        const f2 gd = qd2<qd::kRot2>(g);
+        const f2 B1 = k.R[2];
+        k.R[2] = B1 + cmulc(hd, G);
+        G = G + cmulc(gd, B1);
+    }
+    {   // column c+4 (lane c+3); row 0 only
+        const f2 hr = qd2<qd::kRot1>(h);
+        const f2 hd = hr * m4;
+        const f2 B1 = k.R[3];
+        k.R[3] = B1 + cmulc(hd, G);
+        G = G + cmulc(gr, B1);
+    }
+    // next step's columns: C[d-2](c) = R[d-1](c+1-d); the lanes with no such
+    // row read a padding entry of R (zero) through the rotation
+    k.C[0] = qd2<qd::kRot1>(k.R[1]);
+    k.C[1] = qd2<qd::kRot2>(k.R[2]);
+    k.C[2] = qd2<qd::kRot3>(k.R[3]);
+    // update_eq: error *= kalman_y (y[4], lane 3); eq[i] += error * conj(g[i])
+    const float y4 = qdf<qd::kB3>(yo);
+    const f2 e = f2{er, vi} * y4;
+    k.eqr = k.eqr + cmulc(e, G);     // row c's final gain
+    k.eq4 = k.eq4 + cmulc(e, g);     // lane 3: g[4] (row 4 has no updates)
+    return er;
+}
+
+// x[index+t] at step 0: X[d] = x[c+1-d] = window slot c+2-d (slot k+1 = dec[mi+k])
+__device__ __forceinline__ void qload_x0(const f2* wp2, int c, f2 (&X)[5]) {
+#pragma unroll
+    for (int d = 0; d < 5; d++) X[d] = d <= c + 1 ? wp2[c + 2 - d] : f2{0.0f, 0.0f};
+}
+
+template <bool EXACT>
+__device__ __forceinline__ int qtrain(QKal& k, f2 (&X)[5], const f2* wl, int c, bool& bad) {
+    int matches = 0;
+#pragma unroll QPSK_TRAIN_UNROLL
+    for (int i = 0; i < QK_NPRE; i++) {
+        const f2 nx = wl[i + 1];                   // x[c+1] of the next step
+        const unsigned long long m = i < 64 ? kPreLo : kPreHi;
+        const float ref = ((m >> (i & 63)) & 1ull) ? 1.0f : -1.0f;
+        const float er = qstep<EXACT>(k, X, ref, c, bad);
+        if (er * ref > 0.0f) matches++;
+#pragma unroll
+        for (int t = 4; t > 0; t--) X[t] = X[t - 1];
+        X[0] = nx;
+    }
+    return matches;
+}
+
+// back_frame() for a quad per channel: every lane of the quad has the same
+// matches / valid / rt; the quad's lane 0 writes the per-channel outputs.
+template <typename RtFn>
+__device__ __forceinline__ void back_frame_quad(const RxArgs& a, int ch, bool live, int n, int mi,
+                                                RtFn get_rt, const float2* win, int* rt_next) {
+    const int c = lane_id() & 3;
+    const bool lead = c == 0;
+    const f2* wp2 = reinterpret_cast<const f2*>(win);
+    QKal k = qkal_reset();
+    f2 X[5];
+    qload_x0(wp2, c, X);
+    bool bad = (a.roles & kForceExact) != 0;
+    int matches = qtrain<false>(k, X, wp2 + c + 2, c, bad);
+    if (__builtin_expect(__ballot(bad) != 0ull, 0)) {   // recompute the frame exactly
+        k = qkal_reset();
+        qload_x0(wp2, c, X);
+        matches = qtrain<true>(k, X, wp2 + c + 2, c, bad);
+    }
+    const bool valid = live && matches > QK_MATCH_MIN;   // src/qpsk.c:196
+    const size_t cf = (size_t)ch * a.F + n;
+    const unsigned long long vm = __ballot(valid && lead);
+    if (vm) {   // gather the quad's state (all lanes take part in the DPP moves)
+        DataJob j;
+        j.k.eq[0] = qd2<qd::kB0>(k.eqr);
+        j.k.eq[1] = qd2<qd::kB1>(k.eqr);
+        j.k.eq[2] = qd2<qd::kB2>(k.eqr);
+        j.k.eq[3] = qd2<qd::kB3>(k.eqr);
+        j.k.eq[4] = qd2<qd::kB3>(k.eq4);
+#define QU(i, jj, CT) j.k.u[uix(i, jj)] = qd2<CT>(k.R[(jj) - (i) - 1])
+        QU(0, 1, qd::kB0); QU(0, 2, qd::kB0); QU(0, 3, qd::kB0); QU(0, 4, qd::kB0);
+        QU(1, 2, qd::kB1); QU(1, 3, qd::kB1); QU(1, 4, qd::kB1);
+        QU(2, 3, qd::kB2); QU(2, 4, qd::kB2);
+        QU(3, 4, qd::kB3);
+#undef QU
+        j.k.d[0] = f2{k.d0, k.d0};
+        const float d1 = qdf<qd::kB0>(k.dc), d2 = qdf<qd::kB1>(k.dc);
+        const float d3 = qdf<qd::kB2>(k.dc), d4 = qdf<qd::kB3>(k.dc);
+        j.k.d[1] = f2{d1, d1};
+        j.k.d[2] = f2{d2, d2};
+        j.k.d[3] = f2{d3, d3};
+        j.k.d[4] = f2{d4, d4};
+        unsigned base = 0;
+        if (lane_id() == 0) base = atomicAdd(a.njobs, (unsigned)__popcll(vm));
+        base = __builtin_amdgcn_readfirstlane(base);
+        if (valid && lead) {
+            const unsigned slot = base + (unsigned)__popcll(vm & ((1ull << lane_id()) - 1ull));
+            j.cf = cf;
+            j.ks = (a.g0 + (unsigned)n) % QK_KS_FRAMES;
+            put_job(a.jobs, a.jcap, slot, j, wp2 + 129);
+        }
+    }
+    if (live && !valid) {   // invalid frame: bits (and soft symbols) are zero
+        uint16_t* bo = reinterpret_cast<uint16_t*>(a.bits + cf * QK_NBITS);
+        for (int ss = c; ss < QK_NDSYM; ss += 4) bo[ss] = 0;
+        if (a.soft) {
+            float2* so = a.soft + cf * QK_NDSYM;
+            for (int ss = c; ss < QK_NDSYM; ss += 4) so[ss] = make_float2(0.0f, 0.0f);
+        }
+    }
+    const int rt = get_rt();
+    const int rtn = valid ? mi + QK_NPRE : rt;    // src/qpsk.c:219
+    if (lead) *rt_next = rtn;
+    if (live && lead) {
+        a.valid[cf] = valid ? 1 : 0;
+        if (a.trace)
+            *reinterpret_cast<int4*>(a.trace + cf * 4) = make_int4(mi, matches, valid ? 1 : 0, rtn);
+    }
+}
+
 // 31 x data_eq + qpsk_demod (src/equalizer.c:64-90, src/qpsk.c:268-271) from
 // the job's window samples xs; returns the raw dibits (bit 2s = Q, 2s+1 = I).
 // Decisions collect in a register; the caller stores the 62 bytes after the
@@ -906,15 +1150,23 @@ __global__ void __launch_bounds__(256) rx_data_kernel(const float4* jobs, unsign
 // W (DUAL only): channels per group, 64, 32 or 16.  A narrower group leaves
 // back lanes idle but spreads a small batch over more CUs and gives each front
 // wave fewer channels per frame, which shortens the front half of the chain.
-template <int G, int FP, int MODE, bool DUAL, int W = QK_GROUP>
-__global__ void __launch_bounds__(64 * G * ((DUAL ? 2 : 1) + FP), 3) rx_kernel(
+//
+// QUAD (DUAL, G == 1 only): the back waves hold a quad of lanes per channel
+// (back_frame_quad), 16 channels per wave, W / 16 waves per frame chain.
+template <int G, int FP, int MODE, bool DUAL, int W, bool QUAD>
+constexpr int kBackWavesOf = DUAL ? 2 * G * (QUAD ? W / 16 : 1) : G;
+
+template <int G, int FP, int MODE, bool DUAL, int W = QK_GROUP, bool QUAD = false>
+__global__ void __launch_bounds__(64 * (kBackWavesOf<G, FP, MODE, DUAL, W, QUAD> + G * FP), 3) rx_kernel(
     const int16_t* in, int16_t* hist, const float2* ptab, const unsigned long long* ks,
     float2* win0, float2* win1, int* mi0, int* mi1, int* rt0, int* rt1, uint8_t* bits,
     uint8_t* valid, int32_t* trace, float2* soft, float4* jobs, unsigned* njobs, int nch, int F,
     unsigned g0, int roles, const float* fft_tab, unsigned long long jcap, int* err) {
     static_assert(W == QK_GROUP || (DUAL && G == 1 && W % FP == 0 && W <= QK_GROUP), "group width");
+    static_assert(!QUAD || (DUAL && G == 1 && W % 16 == 0), "quad backs: dual chain, one group");
     constexpr int kGroups = G, kFrontPer = FP;
-    constexpr int kBackWaves = DUAL ? 2 * kGroups : kGroups;
+    constexpr int kBackWaves = kBackWavesOf<G, FP, MODE, DUAL, W, QUAD>;
+    constexpr int kChainWaves = QUAD ? W / 16 : 1;     // back waves per frame chain and group
     constexpr int kFrontCh = W / kFrontPer;            // channels per front wave
     constexpr int kFrontWaves = kGroups * kFrontPer;
     constexpr int kBlock = 64 * (kBackWaves + kFrontWaves);
@@ -951,12 +1203,17 @@ __global__ void __launch_bounds__(64 * G * ((DUAL ? 2 : 1) + FP), 3) rx_kernel(
     if (threadIdx.x < 2 * kGroups) (&bseq[0][0])[threadIdx.x] = (&fcnt[0][0])[threadIdx.x] = 0;
     __syncthreads();
     if constexpr (DUAL) {
+        // bseq[gi][p]: frames of parity p decided, summed over the chain's back
+        // waves; frame m is decided by all of them once it reaches this
+        auto decided = [](int m) { return kChainWaves * (m / 2 + 1); };
         if (wave < kBackWaves) {
-            // ---------------------------------------------------- back of group wave/2,
-            // frames n = wave mod 2
-            const int gi = wave >> 1;
-            const int ch = (grp0 + gi) * W + lane;
-            const bool live = lane < W && ch < a.nch;
+            // ---------------------------------------------------- back of group
+            // (wave >> 1) / kChainWaves, frames n = wave mod 2
+            const int gi = (wave >> 1) / kChainWaves;
+            // channel of this lane within the group: the lane, or its quad
+            const int idx = QUAD ? 16 * ((wave >> 1) % kChainWaves) + (lane >> 2) : lane;
+            const int ch = (grp0 + gi) * W + idx;
+            const bool live = idx < W && ch < a.nch;
             if (((a.roles >> 4) & 3) == 2) __builtin_amdgcn_s_setprio(2);
             // tests (roles bit kDebugStall): one wait that cannot end, on the
             // first back wave of workgroup 0, with a short bound
@@ -966,14 +1223,17 @@ __global__ void __launch_bounds__(64 * G * ((DUAL ? 2 : 1) + FP), 3) rx_kernel(
                 const int p = n & 1;
                 // front(n-1) done by every front wave of the group: window n and mi_n
                 if (n > 0) spin_wait(&fcnt[gi][p ^ 1], kFrontPer * ((n - 1) / 2 + 1), a.err);
-                back_frame(a, live ? ch : 0, live, n, mi_s[gi][p][lane],
-                           [&] {   // rx_timing of frame n = the decision of frame n-1
-                               if (n > 0) spin_wait(&bseq[gi][p ^ 1], n, a.err);
-                               return rt_s[gi][p][lane];
-                           },
-                           win_of(a, a.g0 + (unsigned)n) + (size_t)(live ? ch : 0) * kWinStride,
-                           &rt_s[gi][p ^ 1][lane]);
-                signal_set(&bseq[gi][p], n + 1, lane);
+                const int mi = mi_s[gi][p][idx];
+                auto get_rt = [&] {   // rx_timing of frame n = the decision of frame n-1
+                    if (n > 0) spin_wait(&bseq[gi][p ^ 1], decided(n - 1), a.err);
+                    return rt_s[gi][p][idx];
+                };
+                const float2* wn = win_of(a, a.g0 + (unsigned)n) + (size_t)(live ? ch : 0) * kWinStride;
+                if constexpr (QUAD)
+                    back_frame_quad(a, live ? ch : 0, live, n, mi, get_rt, wn, &rt_s[gi][p ^ 1][idx]);
+                else
+                    back_frame(a, live ? ch : 0, live, n, mi, get_rt, wn, &rt_s[gi][p ^ 1][idx]);
+                signal_add(&bseq[gi][p], 1, lane);
             }
         } else {
             // ---------------------------------------------------- front
@@ -1001,7 +1261,7 @@ __global__ void __launch_bounds__(64 * G * ((DUAL ? 2 : 1) + FP), 3) rx_kernel(
                 float2* wout = win_of(a, g + 1u);
                 // back(n-1) done: rx_timing of frame n, and window n+1's buffer
                 // (window n-1) and mi_s[p ^ 1] (mi_{n-1}) are free
-                if (n > 0) spin_wait(&bseq[gi][p ^ 1], n, a.err);
+                if (n > 0) spin_wait(&bseq[gi][p ^ 1], decided(n - 1), a.err);
                 int pmi = 0;
                 for (int c = 0; c < nlive; c++) {
                     const int ch = ch0 + c;
@@ -1028,12 +1288,13 @@ __global__ void __launch_bounds__(64 * G * ((DUAL ? 2 : 1) + FP), 3) rx_kernel(
         }
         __syncthreads();
         if (wave < kBackWaves && (wave & 1) == 0) {   // state after the call's last frame
-            const int gi = wave >> 1;
-            const int ch = (grp0 + gi) * W + lane;
-            if (lane < W && ch < a.nch) {
+            const int gi = (wave >> 1) / kChainWaves;
+            const int idx = QUAD ? 16 * ((wave >> 1) % kChainWaves) + (lane >> 2) : lane;
+            const int ch = (grp0 + gi) * W + idx;
+            if (idx < W && ch < a.nch && (!QUAD || (lane & 3) == 0)) {
                 const unsigned ge = a.g0 + (unsigned)a.F;
-                mi_of(a, ge)[ch] = mi_s[gi][a.F & 1][lane];
-                rt_of(a, ge)[ch] = rt_s[gi][a.F & 1][lane];
+                mi_of(a, ge)[ch] = mi_s[gi][a.F & 1][idx];
+                rt_of(a, ge)[ch] = rt_s[gi][a.F & 1][idx];
             }
         }
         return;
@@ -1131,7 +1392,7 @@ float bits2f(uint32_t u) {
 
 // rx_kernel instantiations (pick_shape below)
 struct Shape {
-    enum Kind { k4x2, k2x4d, k1x8d16, k1x8d32, k1x8d64 };
+    enum Kind { k4x2, k2x4d, k1x8d16, k1x8d32, k1x8d64, k1x8q16, k1x8q32, k1x8q64 };
     int kind;
     int roles;
 };
@@ -1179,6 +1440,7 @@ struct qpsk_ctx {
     int ncu = 256;              // compute units of the device
     int shape = -1;             // Shape::Kind forced by QPSK_SHAPE (A/B runs); -1: by batch size
     int width = 0;              // dual-chain group width forced by QPSK_WIDTH; 0: by batch size
+    int quad = -1;              // quad-per-channel backs forced on/off by QPSK_QUAD; -1: by width
     int* d_err = nullptr;       // device error word (kErrStall), cleared by qpsk_rx_sync
     hipStream_t last = nullptr; // stream of the latest qpsk_rx_batch_device call
     float pend_ms[2] = {0.0f, 0.0f};
@@ -1345,6 +1607,7 @@ extern "C" qpsk_ctx* qpsk_rx_create_mode(int device, int nch, int mode, int* err
         const int v = atoi(w);
         c->width = (v == 16 || v == 32 || v == 64) ? v : 0;
     }
+    if (const char* qv = getenv("QPSK_QUAD")) c->quad = atoi(qv) != 0;
     if (const char* sh = getenv("QPSK_SHAPE")) {
         c->shape = !strcmp(sh, "4x2") ? Shape::k4x2 : !strcmp(sh, "2x4d") ? Shape::k2x4d
                  : !strcmp(sh, "1x8") ? Shape::k1x8d64 : -1;
@@ -1409,8 +1672,13 @@ static Shape pick_shape(const qpsk_ctx* c) {
         const int W = c->width > 0 ? c->width
                     : (size_t)c->nch <= (size_t)16 * c->ncu ? 16
                     : (size_t)c->nch <= (size_t)32 * c->ncu ? 32 : 64;
-        sh.kind = W == 16 ? Shape::k1x8d16 : W == 32 ? Shape::k1x8d32 : Shape::k1x8d64;
-        if (W == 64) sh.roles = (sh.roles & ~((3 << 4) | (15 << 16))) | (2 << 4) | (2 << 16);
+        const bool quad = c->quad >= 0 ? c->quad != 0 : W <= 32;
+        if (quad) {
+            sh.kind = W == 16 ? Shape::k1x8q16 : W == 32 ? Shape::k1x8q32 : Shape::k1x8q64;
+        } else {
+            sh.kind = W == 16 ? Shape::k1x8d16 : W == 32 ? Shape::k1x8d32 : Shape::k1x8d64;
+            if (W == 64) sh.roles = (sh.roles & ~((3 << 4) | (15 << 16))) | (2 << 4) | (2 << 16);
+        }
     }
     return sh;
 }
@@ -1454,10 +1722,11 @@ extern "C" int qpsk_rx_batch_device(qpsk_ctx* c, const int16_t* d_in, int F, uin
     }
     const int parity = (int)(c->calls & 1u);
     const Shape sh = pick_shape(c);
-#define QPSK_LAUNCH(GG, FF, MM, DD, WW)                                                        \
-    hipLaunchKernelGGL((rx_kernel<GG, FF, MM, DD, WW>),                                        \
+#define QPSK_LAUNCH(GG, FF, MM, DD, WW, QQ)                                                    \
+    hipLaunchKernelGGL((rx_kernel<GG, FF, MM, DD, WW, QQ>),                                    \
                        dim3((unsigned)((c->nch + (size_t)GG * WW - 1) / ((size_t)GG * WW))),   \
-                       dim3(64 * GG * ((DD ? 2 : 1) + FF)), 0, s, d_in, c->d_hist, c->d_ptab,  \
+                       dim3(64 * (kBackWavesOf<GG, FF, MM, DD, WW, QQ> + GG * FF)), 0, s,      \
+                       d_in, c->d_hist, c->d_ptab,                                             \
                        c->d_ks, c->d_win[0], c->d_win[1], c->d_mi[0], c->d_mi[1], c->d_rt[0],  \
                        c->d_rt[1], d_bits, d_valid, d_trace, reinterpret_cast<float2*>(d_soft), \
                        c->d_jobs, c->d_njobs + parity, c->nch, F,                               \
@@ -1466,11 +1735,14 @@ extern "C" int qpsk_rx_batch_device(qpsk_ctx* c, const int16_t* d_in, int F, uin
 #define QPSK_LAUNCH_MODE(MM)                                                                   \
     do {                                                                                       \
         switch (sh.kind) {                                                                     \
-            case Shape::k2x4d: QPSK_LAUNCH(2, 4, MM, true, 64); break;                         \
-            case Shape::k1x8d16: QPSK_LAUNCH(1, 8, MM, true, 16); break;                       \
-            case Shape::k1x8d32: QPSK_LAUNCH(1, 8, MM, true, 32); break;                       \
-            case Shape::k1x8d64: QPSK_LAUNCH(1, 8, MM, true, 64); break;                       \
-            default: QPSK_LAUNCH(4, 2, MM, false, 64); break;                                  \
+            case Shape::k2x4d: QPSK_LAUNCH(2, 4, MM, true, 64, false); break;                  \
+            case Shape::k1x8d16: QPSK_LAUNCH(1, 8, MM, true, 16, false); break;                \
+            case Shape::k1x8d32: QPSK_LAUNCH(1, 8, MM, true, 32, false); break;                \
+            case Shape::k1x8d64: QPSK_LAUNCH(1, 8, MM, true, 64, false); break;                \
+            case Shape::k1x8q16: QPSK_LAUNCH(1, 8, MM, true, 16, true); break;                 \
+            case Shape::k1x8q32: QPSK_LAUNCH(1, 8, MM, true, 32, true); break;                 \
+            case Shape::k1x8q64: QPSK_LAUNCH(1, 8, MM, true, 64, true); break;                 \
+            default: QPSK_LAUNCH(4, 2, MM, false, 64, false); break;                           \
         }                                                                                      \
     } while (0)
     switch (c->mode) {

@@ -235,14 +235,49 @@ def test_every_workgroup_shape(shape, monkeypatch):
     _vs_oracle(x)
 
 
+@pytest.mark.parametrize("quad", ["0", "1"])
 @pytest.mark.parametrize("width", ["16", "32", "64"])
-def test_dual_chain_group_widths(width, monkeypatch):
-    """One group per workgroup runs the dual-chain kernel (two back waves,
-    even/odd frames, LDS progress counters); QPSK_WIDTH forces its group width
-    (channels per workgroup) on one ragged batch.  W = 64 also moves 2 channels
-    between the front waves (pick_shape's split)."""
+def test_dual_chain_group_widths(width, quad, monkeypatch):
+    """One group per workgroup runs the dual-chain kernel (back waves for the
+    even and the odd frames, LDS progress counters); QPSK_WIDTH forces its
+    group width (channels per workgroup) on one ragged batch, QPSK_QUAD the
+    back layout: a lane per channel (W = 64 also moves 2 channels between the
+    front waves, pick_shape's split) or a quad of lanes per channel
+    (back_frame_quad, W / 16 back waves per frame chain)."""
     monkeypatch.setenv("QPSK_WIDTH", width)
+    monkeypatch.setenv("QPSK_QUAD", quad)
     x = oracle.synth(64, 333, 15, 4.0)
+    _vs_oracle(x)
+
+
+@pytest.mark.parametrize("ebn0", [1000.0, 6.0, 0.0])
+def test_quad_back_edges_and_noise(ebn0, monkeypatch):
+    """The quad-per-channel back on saturated, zero and constant channels next
+    to noisy ones (sign-of-zero and padding paths of back_frame_quad), every
+    output exact."""
+    monkeypatch.setenv("QPSK_QUAD", "1")
+    x = oracle.synth(71, 160, 9, ebn0)
+    x[3] = 0
+    x[17] = 32767
+    x[18] = -32768
+    x[40, 2:5] = 0
+    x[77, :, ::2] = 12345
+    _vs_oracle(x)
+
+
+def test_quad_back_exact_division(monkeypatch):
+    """QPSK_FORCE_EXACT on the quad back: the IEEE-division retrain path."""
+    monkeypatch.setenv("QPSK_QUAD", "1")
+    monkeypatch.setenv("QPSK_FORCE_EXACT", "1")
+    x = oracle.synth(72, 100, 8, 4.0)
+    _vs_oracle(x)
+
+
+def test_c4_shard_8192_channels():
+    """The C4 shard at N = 8 (8,192 channels x 32 frames, AWGN), as bench.py
+    --gpus 8 gives each rank, with the shape pick_shape selects (quad backs):
+    every output equals the oracle's."""
+    x = oracle.synth(81, 8192, 32, 6.0)
     _vs_oracle(x)
 
 
