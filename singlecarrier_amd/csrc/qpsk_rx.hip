@@ -720,15 +720,14 @@ __device__ __forceinline__ void load_x0(const float4* wp, f2 (&x)[5]) {
 constexpr int kForceExact = 64;   // roles bit: take the exact-division path (tests)
 constexpr int kDebugStall = 128;  // roles bit: force one progress wait past its bound (tests)
 
-#ifndef QPSK_TRAIN_UNROLL
-#define QPSK_TRAIN_UNROLL 4   // steps per loop iteration (register reuse; A/B knob)
-#endif
-
-// 128 x train_eq (src/equalizer.c:45-58) from the window; returns matches
+// 128 x train_eq (src/equalizer.c:45-58) from the window; returns matches.
+// (The window load one step ahead stays: a 4-step ring loaded an iteration
+// ahead, as qtrain's, changes this loop's schedule to one with ~50 s_nop per
+// step in the 4x2 kernel.)
 template <bool EXACT>
 __device__ __forceinline__ int train(Kal& k, f2 (&x)[5], const f2* wp2, bool& bad) {
     int matches = 0;
-#pragma unroll QPSK_TRAIN_UNROLL
+#pragma unroll 4
     for (int i = 0; i < QK_NPRE; i++) {
         const f2 nx = wp2[i + 6];                  // slot i+6 (next step)
         const unsigned long long m = i < 64 ? kPreLo : kPreHi;
@@ -967,19 +966,33 @@ __device__ __forceinline__ void qload_x0(const f2* wp2, int c, f2 (&X)[5]) {
     for (int d = 0; d < 5; d++) X[d] = d <= c + 1 ? wp2[c + 2 - d] : f2{0.0f, 0.0f};
 }
 
+// Window samples arrive through a 4-step ring loaded one loop iteration (4
+// steps, ~3k cycles) ahead: a load issued one step ahead waited out most of an
+// L2 round trip every step.  wl[s] = x[c+1] of step s; the reads run to step
+// 135, inside the 168-slot window row.
 template <bool EXACT>
 __device__ __forceinline__ int qtrain(QKal& k, f2 (&X)[5], const f2* wl, int c, bool& bad) {
     int matches = 0;
-#pragma unroll QPSK_TRAIN_UNROLL
-    for (int i = 0; i < QK_NPRE; i++) {
-        const f2 nx = wl[i + 1];                   // x[c+1] of the next step
-        const unsigned long long m = i < 64 ? kPreLo : kPreHi;
-        const float ref = ((m >> (i & 63)) & 1ull) ? 1.0f : -1.0f;
-        const float er = qstep<EXACT>(k, X, ref, c, bad);
-        if (er * ref > 0.0f) matches++;
+    f2 B[4];
 #pragma unroll
-        for (int t = 4; t > 0; t--) X[t] = X[t - 1];
-        X[0] = nx;
+    for (int t = 0; t < 4; t++) B[t] = wl[t + 1];
+    for (int i = 0; i < QK_NPRE; i += 4) {
+        f2 Bn[4];
+#pragma unroll
+        for (int t = 0; t < 4; t++) Bn[t] = wl[i + 5 + t];
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            const int st = i + t;
+            const unsigned long long m = st < 64 ? kPreLo : kPreHi;
+            const float ref = ((m >> (st & 63)) & 1ull) ? 1.0f : -1.0f;
+            const float er = qstep<EXACT>(k, X, ref, c, bad);
+            if (er * ref > 0.0f) matches++;
+#pragma unroll
+            for (int d = 4; d > 0; d--) X[d] = X[d - 1];
+            X[0] = B[t];
+        }
+#pragma unroll
+        for (int t = 0; t < 4; t++) B[t] = Bn[t];
     }
     return matches;
 }
@@ -1219,13 +1232,19 @@ __global__ void __launch_bounds__(64 * (kBackWavesOf<G, FP, MODE, DUAL, W, QUAD>
             // first back wave of workgroup 0, with a short bound
             if ((a.roles & kDebugStall) && blockIdx.x == 0 && wave == 0)
                 spin_wait(&fcnt[gi][0], 1 << 30, a.err, 1u << 12);
+            // diagnostic stamps (QPSK_STAMPS): 13 frame work, 14 wait for the
+            // fronts, 15 wait for the other chain's decision
+            STAMP_DECL
             for (int n = wave & 1; n < a.F; n += 2) {
                 const int p = n & 1;
                 // front(n-1) done by every front wave of the group: window n and mi_n
                 if (n > 0) spin_wait(&fcnt[gi][p ^ 1], kFrontPer * ((n - 1) / 2 + 1), a.err);
+                STAMP(14);
                 const int mi = mi_s[gi][p][idx];
                 auto get_rt = [&] {   // rx_timing of frame n = the decision of frame n-1
+                    STAMP(13);
                     if (n > 0) spin_wait(&bseq[gi][p ^ 1], decided(n - 1), a.err);
+                    STAMP(15);
                     return rt_s[gi][p][idx];
                 };
                 const float2* wn = win_of(a, a.g0 + (unsigned)n) + (size_t)(live ? ch : 0) * kWinStride;
@@ -1234,7 +1253,9 @@ __global__ void __launch_bounds__(64 * (kBackWavesOf<G, FP, MODE, DUAL, W, QUAD>
                 else
                     back_frame(a, live ? ch : 0, live, n, mi, get_rt, wn, &rt_s[gi][p ^ 1][idx]);
                 signal_add(&bseq[gi][p], 1, lane);
+                STAMP(13);
             }
+            STAMP_FLUSH();
         } else {
             // ---------------------------------------------------- front
             const int f = wave - kBackWaves;
@@ -1255,6 +1276,10 @@ __global__ void __launch_bounds__(64 * (kBackWavesOf<G, FP, MODE, DUAL, W, QUAD>
             int pf[kPf<DM>];
             if (((a.roles >> 4) & 3) == 1) __builtin_amdgcn_s_setprio(2);
             if (nlive > 0) prefetch<DM>(srcs(a, ch0, 0), lane, pf);
+            // diagnostic stamps (QPSK_STAMPS): 7 wait for the backs, 0 mix,
+            // 1 window store + prefetch, 8-12 front_channel phases, 6 its tail,
+            // 5 signal
+            STAMP_DECL
             for (int n = 0; n < a.F; n++) {
                 const int p = n & 1;
                 const unsigned g = a.g0 + (unsigned)n;
@@ -1262,11 +1287,13 @@ __global__ void __launch_bounds__(64 * (kBackWavesOf<G, FP, MODE, DUAL, W, QUAD>
                 // back(n-1) done: rx_timing of frame n, and window n+1's buffer
                 // (window n-1) and mi_s[p ^ 1] (mi_{n-1}) are free
                 if (n > 0) spin_wait(&bseq[gi][p ^ 1], decided(n - 1), a.err);
+                STAMP(7);
                 int pmi = 0;
                 for (int c = 0; c < nlive; c++) {
                     const int ch = ch0 + c;
                     float2* dcur = decs[f][c % kDecBuf];
                     mix<DM>(lane, pf, g, P, M);
+                    STAMP(0);
                     if (c > 0) store_window(lane, pmi, decs[f][(c - 1) % kDecBuf], wout + (size_t)(ch - 1) * kWinStride);
                     {
                         const bool same = c + 1 < nlive;
@@ -1274,16 +1301,17 @@ __global__ void __launch_bounds__(64 * (kBackWavesOf<G, FP, MODE, DUAL, W, QUAD>
                             prefetch<DM>(srcs(a, same ? ch + 1 : ch0, same ? n : n + 1), lane, pf);
                     }
                     wave_lds_sync();
-#ifdef QPSK_STAMPS
-                    unsigned long long st_acc[16];   // dual-chain shapes are not stamped
-#endif
+                    STAMP(1);
                     pmi = front_channel<MODE>(lane, rt_s[gi][p][cbeg + c], M, dcur, BT FACC_ARG);
                     if (lane == 0) mi_s[gi][p ^ 1][cbeg + c] = pmi;
                     if (c + 1 == nlive) store_window(lane, pmi, dcur, wout + (size_t)ch * kWinStride);
                     wave_lds_sync();
+                    STAMP(6);
                 }
                 signal_add(&fcnt[gi][p], 1, lane);
+                STAMP(5);
             }
+            STAMP_FLUSH();
             carry_history<DM>(a.in, a.hist, a.F, ch0, nlive, lane);
         }
         __syncthreads();
@@ -1392,7 +1420,7 @@ float bits2f(uint32_t u) {
 
 // rx_kernel instantiations (pick_shape below)
 struct Shape {
-    enum Kind { k4x2, k2x4d, k1x8d16, k1x8d32, k1x8d64, k1x8q16, k1x8q32, k1x8q64 };
+    enum Kind { k4x2, k2x4d, k1x8d16, k1x8d32, k1x8d64, k1x8q16, k1x8q32 };
     int kind;
     int roles;
 };
@@ -1441,6 +1469,7 @@ struct qpsk_ctx {
     int shape = -1;             // Shape::Kind forced by QPSK_SHAPE (A/B runs); -1: by batch size
     int width = 0;              // dual-chain group width forced by QPSK_WIDTH; 0: by batch size
     int quad = -1;              // quad-per-channel backs forced on/off by QPSK_QUAD; -1: by width
+    int prio = -1;              // issue priority forced by QPSK_PRIO (0 none, 1 front, 2 back)
     int* d_err = nullptr;       // device error word (kErrStall), cleared by qpsk_rx_sync
     hipStream_t last = nullptr; // stream of the latest qpsk_rx_batch_device call
     float pend_ms[2] = {0.0f, 0.0f};
@@ -1608,6 +1637,8 @@ extern "C" qpsk_ctx* qpsk_rx_create_mode(int device, int nch, int mode, int* err
         c->width = (v == 16 || v == 32 || v == 64) ? v : 0;
     }
     if (const char* qv = getenv("QPSK_QUAD")) c->quad = atoi(qv) != 0;
+    if (const char* pv = getenv("QPSK_PRIO"))
+        c->prio = !strcmp(pv, "none") ? 0 : !strcmp(pv, "front") ? 1 : !strcmp(pv, "back") ? 2 : -1;
     if (const char* sh = getenv("QPSK_SHAPE")) {
         c->shape = !strcmp(sh, "4x2") ? Shape::k4x2 : !strcmp(sh, "2x4d") ? Shape::k2x4d
                  : !strcmp(sh, "1x8") ? Shape::k1x8d64 : -1;
@@ -1672,14 +1703,18 @@ static Shape pick_shape(const qpsk_ctx* c) {
         const int W = c->width > 0 ? c->width
                     : (size_t)c->nch <= (size_t)16 * c->ncu ? 16
                     : (size_t)c->nch <= (size_t)32 * c->ncu ? 32 : 64;
-        const bool quad = c->quad >= 0 ? c->quad != 0 : W <= 32;
+        // quad backs need W / 16 back waves per chain: at W = 64 that is 16
+        // waves per workgroup, whose 128-VGPR budget spills the front; the
+        // lane-per-channel back stays there (profiles/r02_quad_ab.txt)
+        const bool quad = W <= 32 && (c->quad >= 0 ? c->quad != 0 : true);
         if (quad) {
-            sh.kind = W == 16 ? Shape::k1x8q16 : W == 32 ? Shape::k1x8q32 : Shape::k1x8q64;
+            sh.kind = W == 16 ? Shape::k1x8q16 : Shape::k1x8q32;
         } else {
             sh.kind = W == 16 ? Shape::k1x8d16 : W == 32 ? Shape::k1x8d32 : Shape::k1x8d64;
             if (W == 64) sh.roles = (sh.roles & ~((3 << 4) | (15 << 16))) | (2 << 4) | (2 << 16);
         }
     }
+    if (c->prio >= 0) sh.roles = (sh.roles & ~(3 << 4)) | (c->prio << 4);
     return sh;
 }
 
@@ -1741,7 +1776,6 @@ extern "C" int qpsk_rx_batch_device(qpsk_ctx* c, const int16_t* d_in, int F, uin
             case Shape::k1x8d64: QPSK_LAUNCH(1, 8, MM, true, 64, false); break;                \
             case Shape::k1x8q16: QPSK_LAUNCH(1, 8, MM, true, 16, true); break;                 \
             case Shape::k1x8q32: QPSK_LAUNCH(1, 8, MM, true, 32, true); break;                 \
-            case Shape::k1x8q64: QPSK_LAUNCH(1, 8, MM, true, 64, true); break;                 \
             default: QPSK_LAUNCH(4, 2, MM, false, 64, false); break;                           \
         }                                                                                      \
     } while (0)
