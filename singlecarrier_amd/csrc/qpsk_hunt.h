@@ -34,6 +34,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <utility>
+
 #include "qpsk_consts.h"
 
 namespace qhunt {
@@ -84,16 +86,21 @@ __device__ __forceinline__ int tk_index(int j, int comp) {
 }
 
 // T[j] = (RN(dr - di), RN(di + dr)) for j < 255 and T[255] = 0 (multiplied by
-// B = 0 only), written into the TK image.  Lane l handles j = l + 64r.
+// B = 0 only), written into the TK image.  Lane l handles j = 4l .. 4l+3, i.e.
+// column l of all eight rows: the 32 lanes of a ds_write_b32 then hit 32
+// distinct banks (rows are 0 mod 32 dwords apart, so j = l + 64r put four
+// lanes on one bank); dec[4l .. 4l+3] arrive as two 16-B reads.
 __device__ __forceinline__ void store_t(int lane, const float2* dec, float* TK) {
+    const float4* d4 = reinterpret_cast<const float4*>(dec + 4 * lane);
+    const float4 p = d4[0], q = d4[1];
+    const float dr[4] = {p.x, p.z, q.x, q.z}, di[4] = {p.y, p.w, q.y, q.w};
 #pragma unroll
     for (int r = 0; r < 4; r++) {
-        const int j = lane + 64 * r;
+        const int j = 4 * lane + r;
         float tr = 0.0f, ti = 0.0f;
         if (j < 2 * QK_NLAG - 1) {
-            const float2 d = dec[j];
-            tr = d.x - d.y;
-            ti = d.y + d.x;
+            tr = dr[r] - di[r];
+            ti = di[r] + dr[r];
         }
         TK[tk_index(j, 0)] = tr;
         TK[tk_index(j, 1)] = ti;
@@ -139,5 +146,78 @@ __device__ __forceinline__ f4 correlate_bt(int lane, const float* TK, const floa
 // lags held by this lane's fragment: (re, im) = (acc[0], acc[1]) and (acc[2], acc[3])
 __device__ __forceinline__ int lag_lo(int lane) { return 32 * (lane >> 4) + (lane & 15); }
 __device__ __forceinline__ int lag_hi(int lane) { return lag_lo(lane) + 16; }
+
+// ------------------------------------------------------------ VALU form
+// The same k-ordered chains on the vector ALU.  An f32 MFMA occupies its
+// SIMD's VALU for its whole issue time: beside a dependent
+// v_mfma_f32_16x16x4_f32 chain another wave's v_pk_add_f32 stream slows from
+// 5.0 to 13.0 cycles per instruction (profiles/calib/mfma_mix_r02.txt), so
+// the 36 MFMAs per channel (~1,150 SIMD cycles) cost every wave on the SIMD.
+// Here lane l owns lags 2l and 2l+1; step k adds p_k * T[2l+k] and
+// p_k * T[2l+1+k] with one v_pk_add_f32 each ((re, im) packed; p_k = -1 is a
+// negation modifier: RN(acc - T) == fmaf(-1, T, acc)).  One 16-B LDS read of
+// (T[2l+k], T[2l+k+1]) (k even) serves both lags for two steps: 65 reads and
+// 256 packed adds per channel.
+constexpr int kTV = 256;            // float2 per T image (2 KB)
+
+// TV[j] = T[j] = (RN(dr - di), RN(di + dr)) for j < 255, TV[255] = 0.
+// Lane l handles j = l + 64r: 8-B reads and writes at 8-B lane stride.
+__device__ __forceinline__ void store_tv(int lane, const float2* dec, float2* TV) {
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const int j = lane + 64 * r;
+        float tr = 0.0f, ti = 0.0f;
+        if (j < 2 * QK_NLAG - 1) {
+            const float2 d = dec[j];
+            tr = d.x - d.y;
+            ti = d.y + d.x;
+        }
+        TV[j] = make_float2(tr, ti);
+    }
+}
+
+typedef float v2 __attribute__((ext_vector_type(2)));
+
+template <bool NEG>
+__device__ __forceinline__ v2 acc_add(v2 a, v2 t) {
+    v2 r;
+    if (NEG) asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(t));
+    else asm("v_pk_add_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(t));
+    return r;
+}
+
+template <int K>
+__device__ __forceinline__ v2 acc_step(v2 a, v2 t) {
+    constexpr unsigned long long m = K < 64 ? pre_mask(0) : pre_mask(1);
+    return acc_add<((m >> (K & 63)) & 1ull) == 0>(a, t);
+}
+
+template <int... I>
+__device__ __forceinline__ void chain_valu(const f4* src, v2& a0, v2& a1,
+                                           std::integer_sequence<int, I...>) {
+    // step pair (2i, 2i+1): q = (T[2l+2i], T[2l+2i+1]), n = (T[2l+2i+2], ..)
+    f4 q = src[0];
+    auto pair = [&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        const f4 n = src[i + 1];
+        a0 = acc_step<2 * i>(a0, v2{q.x, q.y});
+        a1 = acc_step<2 * i>(a1, v2{q.z, q.w});
+        a0 = acc_step<2 * i + 1>(a0, v2{q.z, q.w});
+        a1 = acc_step<2 * i + 1>(a1, v2{n.x, n.y});
+        q = n;
+    };
+    (pair(std::integral_constant<int, I>{}), ...);
+}
+
+// Returns (re, im) of lag 2l in [0], [1] and of lag 2l+1 in [2], [3].
+__device__ __forceinline__ f4 correlate_valu(int lane, const float2* TV) {
+    const f4* src = reinterpret_cast<const f4*>(TV + 2 * lane);
+    v2 a0 = {0.0f, 0.0f}, a1 = {0.0f, 0.0f};
+    chain_valu(src, a0, a1, std::make_integer_sequence<int, QK_NPRE / 2>{});
+    return f4{a0.x, a0.y, a1.x, a1.y};
+}
+
+__device__ __forceinline__ int lag_lo_valu(int lane) { return 2 * lane; }
+__device__ __forceinline__ int lag_hi_valu(int lane) { return 2 * lane + 1; }
 
 }  // namespace qhunt

@@ -63,6 +63,9 @@ constexpr int kDec = 296;
 #ifndef QPSK_FB
 #define QPSK_FB 15   // FIR samples per LDS batch (A/B knob)
 #endif
+#ifndef QPSK_HUNT_MFMA
+#define QPSK_HUNT_MFMA 1   // 1: hunt on the matrix cores; 0: packed VALU chains (A/B knob)
+#endif
 
 constexpr int kM1 = 1240;
 template <int MODE> struct Cfg;
@@ -279,7 +282,6 @@ __device__ __forceinline__ unsigned wave_max_u32(unsigned v) {
     return (unsigned)__builtin_amdgcn_readlane((int)v, 63);
 }
 
-__device__ __forceinline__ f2 ld2(const float2* p) { return *reinterpret_cast<const f2*>(p); }
 // same, but volatile so the load/store optimizer does not pair it into a
 // ds_read2_b64 (8 LDS cycles per pair vs 2 per ds_read_b64: MI355X_MICROARCH.md)
 typedef __attribute__((address_space(3))) const volatile f2 lds_vf2;
@@ -407,6 +409,9 @@ __device__ __forceinline__ int front_channel(int lane, int rt, float2* M, float2
     }
     FSTAMP(0);
     // Undecimated head F_{n+1}[j] = fir_out'[j], j < 102: lane l makes j = 2l, 2l+1
+    // from M[kM1 + 2l + s], s < 50, read as 16-B sample pairs (lane stride 16 B:
+    // ds_read_b128's lane groups cover the 64 banks once; a b64 read at that
+    // stride is 2-way conflicted)
     if (lane < 51) {
         const float2* b = M + kM1 + 2 * lane;
         f2 y[2] = {{0.0f, 0.0f}, {0.0f, 0.0f}};
@@ -414,7 +419,11 @@ __device__ __forceinline__ int front_channel(int lane, int rt, float2* M, float2
         for (int s0 = 0; s0 < 50; s0 += 10) {
             f2 v[10];
 #pragma unroll
-            for (int j = 0; j < 10; j++) v[j] = ld2(b + s0 + j);
+            for (int j = 0; j < 10; j += 2) {
+                const float4 q = *reinterpret_cast<const float4*>(b + s0 + j);
+                v[j] = f2{q.x, q.y};
+                v[j + 1] = f2{q.z, q.w};
+            }
 #pragma unroll
             for (int j = 0; j < 10; j++) {
                 const int s = s0 + j;
@@ -425,16 +434,14 @@ __device__ __forceinline__ int front_channel(int lane, int rt, float2* M, float2
                 }
             }
         }
-#pragma unroll
-        for (int m = 0; m < 2; m++) {
-            const f2 o = y[m] * QK_GAIN;
-            dec[QK_NDEC + 2 * lane + m] = make_float2(o.x, o.y);
-        }
+        const f2 o0 = y[0] * QK_GAIN, o1 = y[1] * QK_GAIN;   // one 16-B store
+        *reinterpret_cast<float4*>(dec + QK_NDEC + 2 * lane) = make_float4(o0.x, o0.y, o1.x, o1.y);
     }
     }
     wave_lds_sync();
     FSTAMP(1);
     if constexpr ((MODE & 2) != 0) return fft_hunt(lane, M, dec, BT);
+#if QPSK_HUNT_MFMA
     // correlate (src/qpsk.c:88-96) for all 128 lags on the matrix cores
     // (qpsk_hunt.h: bit-identical k-ordered chain); the TK image reuses M.
     float* TK = reinterpret_cast<float*>(M);
@@ -443,6 +450,20 @@ __device__ __forceinline__ int front_channel(int lane, int rt, float2* M, float2
     FSTAMP(2);
     const qhunt::f4 acc = qhunt::correlate_bt(lane, TK, BT);
     FSTAMP(3);
+#define QPSK_LAG_LO qhunt::lag_lo
+#define QPSK_LAG_HI qhunt::lag_hi
+#else
+    // correlate (src/qpsk.c:88-96) for all 128 lags as packed VALU chains
+    // (qpsk_hunt.h correlate_valu: the same k-ordered sums); T reuses M.
+    float2* TV = M;
+    qhunt::store_tv(lane, dec, TV);
+    wave_lds_sync();
+    FSTAMP(2);
+    const qhunt::f4 acc = qhunt::correlate_valu(lane, TV);
+    FSTAMP(3);
+#define QPSK_LAG_LO qhunt::lag_lo_valu
+#define QPSK_LAG_HI qhunt::lag_hi_valu
+#endif
     const float r0 = acc[0], i0 = acc[1], r1 = acc[2], i1 = acc[3];
     const float c0 = r0 * r0 + i0 * i0;    // cnormf, src/qpsk.c:75-80
     const float c1 = r1 * r1 + i1 * i1;
@@ -457,8 +478,10 @@ __device__ __forceinline__ int front_channel(int lane, int rt, float2* M, float2
     FSTAMP(4);
     if (km == 0u) return 0;
     const unsigned long long m0 = __ballot(k0 == km), m1 = __ballot(k1 == km);
-    const int i0x = m0 ? qhunt::lag_lo(__ffsll((long long)m0) - 1) : 1 << 20;
-    const int i1x = m1 ? qhunt::lag_hi(__ffsll((long long)m1) - 1) : 1 << 20;
+    const int i0x = m0 ? QPSK_LAG_LO(__ffsll((long long)m0) - 1) : 1 << 20;
+    const int i1x = m1 ? QPSK_LAG_HI(__ffsll((long long)m1) - 1) : 1 << 20;
+#undef QPSK_LAG_LO
+#undef QPSK_LAG_HI
     return min(i0x, i1x);
 }
 
