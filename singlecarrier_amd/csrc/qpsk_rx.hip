@@ -103,9 +103,6 @@ struct RxArgs {
                              // issue priority boost (0 none, 1 front, 2 back);
                              // bits 8-15: front stagger; bits 16-19: front split
     int* err;                // device error word (kErrStall)
-    float2* wspec;           // SPEC: windows [4 frame slots][2 candidates][nslot][168]
-    size_t wplane;           //       floats2 per (slot, candidate) plane: nslot * 168
-    int* vhist;              //       [nslot] valid flags of the call's last two frames
 };
 
 // Diagnostic build only (-DQPSK_STAMPS): per-phase cycle sums of the front
@@ -406,9 +403,8 @@ __device__ __forceinline__ void fir_dec(int lane, int rt, const float2* M, float
 // Undecimated head F_{n+1}[j] = fir_out'[j], j < 102: lane l makes j = 2l, 2l+1
 // from M[kM1 + 2l + s], s < 50, read as 16-B sample pairs (lane stride 16 B:
 // ds_read_b128's lane groups cover the 64 banks once; a b64 read at that
-// stride is 2-way conflicted).  It does not depend on rx_timing: the
-// speculative front (rx_kernel<.., SPEC>) writes it into both candidates' dec.
-__device__ __forceinline__ void fir_head(int lane, const float2* M, float2* dec, float2* dec2) {
+// stride is 2-way conflicted).  It does not depend on rx_timing.
+__device__ __forceinline__ void fir_head(int lane, const float2* M, float2* dec) {
     if (lane < 51) {
         const float2* b = M + kM1 + 2 * lane;
         f2 y[2] = {{0.0f, 0.0f}, {0.0f, 0.0f}};
@@ -432,9 +428,7 @@ __device__ __forceinline__ void fir_head(int lane, const float2* M, float2* dec,
             }
         }
         const f2 o0 = y[0] * QK_GAIN, o1 = y[1] * QK_GAIN;   // one 16-B store
-        const float4 o = make_float4(o0.x, o0.y, o1.x, o1.y);
-        *reinterpret_cast<float4*>(dec + QK_NDEC + 2 * lane) = o;
-        if (dec2) *reinterpret_cast<float4*>(dec2 + QK_NDEC + 2 * lane) = o;
+        *reinterpret_cast<float4*>(dec + QK_NDEC + 2 * lane) = make_float4(o0.x, o0.y, o1.x, o1.y);
     }
 }
 
@@ -502,7 +496,7 @@ __device__ __forceinline__ int front_channel(int lane, int rt, float2* M, float2
     } else {
         fir_dec(lane, rt, M, dec);
         FSTAMP(0);
-        fir_head(lane, M, dec, nullptr);
+        fir_head(lane, M, dec);
     }
     wave_lds_sync();
     FSTAMP(1);
@@ -766,7 +760,6 @@ __device__ __forceinline__ void load_x0(const float4* wp, f2 (&x)[5]) {
 
 constexpr int kForceExact = 64;   // roles bit: take the exact-division path (tests)
 constexpr int kDebugStall = 128;  // roles bit: force one progress wait past its bound (tests)
-constexpr int kNoSpec = 1 << 20;  // roles bit: SPEC kernel without speculation (A/B)
 
 // 128 x train_eq (src/equalizer.c:45-58) from the window; returns matches.
 // (The window load one step ahead stays: a 4-step ring loaded an iteration
@@ -1049,8 +1042,7 @@ __device__ __forceinline__ int qtrain(QKal& k, f2 (&X)[5], const f2* wl, int c, 
 // matches / valid / rt; the quad's lane 0 writes the per-channel outputs.
 template <typename RtFn>
 __device__ __forceinline__ void back_frame_quad(const RxArgs& a, int ch, bool live, int n, int mi,
-                                                RtFn get_rt, const float2* win, int* rt_next,
-                                                int* valid_out = nullptr) {
+                                                RtFn get_rt, const float2* win, int* rt_next) {
     const int c = lane_id() & 3;
     const bool lead = c == 0;
     const f2* wp2 = reinterpret_cast<const f2*>(win);
@@ -1108,7 +1100,6 @@ __device__ __forceinline__ void back_frame_quad(const RxArgs& a, int ch, bool li
     const int rt = get_rt();
     const int rtn = valid ? mi + QK_NPRE : rt;    // src/qpsk.c:219
     if (lead) *rt_next = rtn;
-    if (lead && valid_out) *valid_out = valid ? 1 : 0;
     if (live && lead) {
         a.valid[cf] = valid ? 1 : 0;
         if (a.trace)
@@ -1218,33 +1209,23 @@ __global__ void __launch_bounds__(256) rx_data_kernel(const float4* jobs, unsign
 // (back_frame_quad), 16 channels per wave, W / 16 waves per frame chain.
 template <int G, int FP, int MODE, bool DUAL, int W, bool QUAD>
 constexpr int kBackWavesOf = DUAL ? 2 * G * (QUAD ? W / 16 : 1) : G;
-// ISO (SPEC kernel): 12 waves; waves 4q + {0, 1} are back waves (idle past
-// the back count), waves 4q + {2, 3} the FP = 6 front waves, so back and front
-// waves never share a SIMD (a workgroup's wave w runs on SIMD (s0 + w) mod 4 in
-// the cyclic order, MI355X_MICROARCH.md LDS section)
-template <int G, int FP, int MODE, bool DUAL, int W, bool QUAD, bool ISO>
-constexpr int kBlockWavesOf = ISO ? 12 : kBackWavesOf<G, FP, MODE, DUAL, W, QUAD> + G * FP;
 
-template <int G, int FP, int MODE, bool DUAL, int W = QK_GROUP, bool QUAD = false, bool SPEC = false,
-          bool ISO = false>
-__global__ void __launch_bounds__(64 * (kBlockWavesOf<G, FP, MODE, DUAL, W, QUAD, ISO>), 3) rx_kernel(
+template <int G, int FP, int MODE, bool DUAL, int W = QK_GROUP, bool QUAD = false>
+__global__ void __launch_bounds__(64 * (kBackWavesOf<G, FP, MODE, DUAL, W, QUAD> + G * FP), 3) rx_kernel(
     const int16_t* in, int16_t* hist, const float2* ptab, const unsigned long long* ks,
     float2* win0, float2* win1, int* mi0, int* mi1, int* rt0, int* rt1, uint8_t* bits,
     uint8_t* valid, int32_t* trace, float2* soft, float4* jobs, unsigned* njobs, int nch, int F,
-    unsigned g0, int roles, const float* fft_tab, unsigned long long jcap, int* err,
-    float2* wspec, unsigned long long wplane, int* vhist) {
-    static_assert(W == QK_GROUP || (DUAL && G == 1 && (W % FP == 0 || ISO) && W <= QK_GROUP), "group width");
-    static_assert(!ISO || (SPEC && FP == 6), "isolated roles: SPEC kernel, 6 front waves");
+    unsigned g0, int roles, const float* fft_tab, unsigned long long jcap, int* err) {
+    static_assert(W == QK_GROUP || (DUAL && G == 1 && W % FP == 0 && W <= QK_GROUP), "group width");
     static_assert(!QUAD || (DUAL && G == 1 && W % 16 == 0), "quad backs: dual chain, one group");
-    static_assert(!SPEC || (QUAD && MODE == 0), "speculative fronts: quad backs, reference mode");
     constexpr int kGroups = G, kFrontPer = FP;
     constexpr int kBackWaves = kBackWavesOf<G, FP, MODE, DUAL, W, QUAD>;
     constexpr int kChainWaves = QUAD ? W / 16 : 1;     // back waves per frame chain and group
     constexpr int kFrontCh = W / kFrontPer;            // channels per front wave
     constexpr int kFrontWaves = kGroups * kFrontPer;
-    constexpr int kBlock = 64 * kBlockWavesOf<G, FP, MODE, DUAL, W, QUAD, ISO>;
+    constexpr int kBlock = 64 * (kBackWaves + kFrontWaves);
     const RxArgs a{in, hist, ptab, ks, win0, win1, mi0, mi1, rt0, rt1, bits, valid, trace, soft,
-                   jobs, njobs, nch, F, g0, (size_t)jcap, roles, err, wspec, (size_t)wplane, vhist};
+                   jobs, njobs, nch, F, g0, (size_t)jcap, roles, err};
     __shared__ __attribute__((aligned(16))) float2 P[QK_FRAME];
     constexpr int DM = MODE & 1;   // decimation semantics; MODE & 2: FFT hunt
     constexpr int kM = Cfg<DM>::kM, kDecBuf = Cfg<DM>::kDecBuf;
@@ -1254,10 +1235,6 @@ __global__ void __launch_bounds__(64 * (kBlockWavesOf<G, FP, MODE, DUAL, W, QUAD
     // hunt tables: the MFMA correlator's B, or the FFT hunt's twiddles / Q / permutation
     __shared__ __attribute__((aligned(16))) float BT[(MODE & 2) ? kFftHT : qhunt::kBT];
     __shared__ int bseq[kGroups][2], fcnt[kGroups][2];   // DUAL progress counters, per group
-    // SPEC state by frame index k mod 4 (one group): both candidates' preamble
-    // positions, rx_timing, valid flags
-    constexpr int kSW = SPEC ? W : 1;
-    __shared__ int sv_mi[4][2][kSW], sv_rt[4][kSW], sv_val[4][kSW];
     const int lane = threadIdx.x & 63;
     // wave-uniform by construction; readfirstlane tells the compiler, so every
     // per-wave index and pointer below lives in SGPRs
@@ -1272,165 +1249,13 @@ __global__ void __launch_bounds__(64 * (kBlockWavesOf<G, FP, MODE, DUAL, W, QUAD
     }
     if (wave < kGroups) {   // per-channel state of the groups at the call's first frame
         const int ch = (grp0 + wave) * W + lane;
-        if constexpr (SPEC) {
-            if (lane < W) {
-                const bool in = ch < a.nch;
-                const int mi = in ? mi_of(a, a.g0)[ch] : 0, vh = in ? a.vhist[ch] : 0;
-                sv_mi[0][0][lane] = sv_mi[0][1][lane] = mi;
-                sv_rt[0][lane] = in ? rt_of(a, a.g0)[ch] : QK_RT0;
-                sv_val[2][lane] = vh & 1;          // valid of frame -2
-                sv_val[3][lane] = (vh >> 1) & 1;   // valid of frame -1
-            }
-        } else if (lane < W && ch < a.nch) {
+        if (lane < W && ch < a.nch) {
             mi_s[wave][0][lane] = mi_of(a, a.g0)[ch];
             rt_s[wave][0][lane] = rt_of(a, a.g0)[ch];
         }
     }
     if (threadIdx.x < 2 * kGroups) (&bseq[0][0])[threadIdx.x] = (&fcnt[0][0])[threadIdx.x] = 0;
     __syncthreads();
-    if constexpr (SPEC) {
-        // Speculative fronts (small batches; DESIGN.md "Speculative fronts").
-        // rx_timing of frame n is rt_n = valid_{n-1} ? mi_{n-1} + 128 : rt_{n-1}
-        // (src/qpsk.c:196-219), so front(n) needs only decision n-2 (rt_{n-1})
-        // once it computes BOTH candidates: A = mi_{n-1} + 128 (slot 0) and
-        // B = rt_{n-1} (slot 1), each a full D_n, hunt and window (one, written
-        // to both slots, when A == B).  The back of frame n+1 runs on the same
-        // chain as frame n-1 and selects slot valid_{n-1} ? 0 : 1 itself, so
-        // no front sits between two trainings of a chain.  Every output is
-        // that of the selected candidate, i.e. exactly the reference's.
-        // State by frame k mod 4: sv_mi[k][cand] (mi_k), sv_rt[k] (rt_k, by
-        // back(k-1)), sv_val[k] (valid_k, by back(k)); windows of global frame g
-        // in wspec plane (g mod 4, cand).  A slot is rewritten 4 frames later,
-        // after every reader of it has been decided (front(n) waits for
-        // decision n-2, which follows decision n-3).
-        // roles bit kNoSpec: the same kernel without speculation (front(n)
-        // waits for decision n-1 and computes rt_n's candidate only)
-        auto decided = [](int m) { return kChainWaves * (m / 2 + 1); };
-        const bool nospec = (a.roles & kNoSpec) != 0;
-        int bw = -1, f = -1;   // back wave index, front wave index (ISO: some waves idle)
-        if constexpr (ISO) {
-            const int r = wave & 3, q = wave >> 2;
-            if (r < 2) bw = 2 * q + r < kBackWaves ? 2 * q + r : -1;
-            else f = 2 * q + r - 2;
-        } else {
-            if (wave < kBackWaves) bw = wave;
-            else f = wave - kBackWaves;
-        }
-        if (bw >= 0) {
-            const int idx = 16 * ((bw >> 1) % kChainWaves) + (lane >> 2);
-            const int ch = grp0 * W + idx;
-            const bool live = idx < W && ch < a.nch;
-            if (((a.roles >> 4) & 3) == 2) __builtin_amdgcn_s_setprio(2);
-            if ((a.roles & kDebugStall) && blockIdx.x == 0 && bw == 0)
-                spin_wait(&fcnt[0][0], 1 << 30, a.err, 1u << 12);
-            STAMP_DECL
-            for (int k = bw & 1; k < a.F; k += 2) {
-                // front(k-1) done by every front wave: both candidates of window k
-                if (k > 0) spin_wait(&fcnt[0][(k - 1) & 1], kFrontPer * ((k - 1) / 2 + 1), a.err);
-                STAMP(14);
-                // valid_{k-2}: this chain's own previous decision
-                const int cand = (nospec || sv_val[(k + 2) & 3][idx]) ? 0 : 1;
-                const int mi = sv_mi[k & 3][cand][idx];
-                auto get_rt = [&] {   // rt_k = the decision of frame k-1 (other chain)
-                    STAMP(13);
-                    if (k > 0) spin_wait(&bseq[0][(k - 1) & 1], decided(k - 1), a.err);
-                    STAMP(15);
-                    return sv_rt[k & 3][idx];
-                };
-                const unsigned g = a.g0 + (unsigned)k;
-                const float2* wn = a.wspec + (size_t)((g & 3u) * 2u + (unsigned)cand) * a.wplane +
-                                   (size_t)(live ? ch : 0) * kWinStride;
-                back_frame_quad(a, live ? ch : 0, live, k, mi, get_rt, wn, &sv_rt[(k + 1) & 3][idx],
-                                &sv_val[k & 3][idx]);
-                signal_add(&bseq[0][k & 1], 1, lane);
-                STAMP(13);
-            }
-            STAMP_FLUSH();
-        } else if (f >= 0) {
-            constexpr int kQ = W / kFrontPer, kR = W % kFrontPer;   // channels per front wave
-            const int cbeg = f * kQ + min(f, kR);
-            const int ch0 = grp0 * W + cbeg;
-            const int nlive = max(0, min(kQ + (f < kR ? 1 : 0), a.nch - ch0));
-            float2* M = Ms[f];
-            float2* dA = decs[f][0];
-            float2* dB = decs[f][1];
-            int pf[kPf<DM>];
-            if (((a.roles >> 4) & 3) == 1) __builtin_amdgcn_s_setprio(2);
-            if (nlive > 0) prefetch<DM>(srcs(a, ch0, 0), lane, pf);
-            STAMP_DECL
-            for (int n = 0; n < a.F; n++) {
-                const unsigned g = a.g0 + (unsigned)n;
-                // decision n-2 (same parity as n): rt_{n-1}, and every reader of
-                // the slots this frame rewrites is done
-                if (nospec) {
-                    if (n >= 1) spin_wait(&bseq[0][(n - 1) & 1], decided(n - 1), a.err);
-                } else if (n >= 2) {
-                    spin_wait(&bseq[0][n & 1], decided(n - 2), a.err);
-                }
-                STAMP(7);
-                float2* w0 = a.wspec + (size_t)(((g + 1u) & 3u) * 2u) * a.wplane;
-                float2* w1 = w0 + a.wplane;
-                for (int c = 0; c < nlive; c++) {
-                    const int ch = ch0 + c, ci = cbeg + c;
-                    mix<DM>(lane, pf, g, P, M);
-                    STAMP(0);
-                    {
-                        const bool same = c + 1 < nlive;
-                        if (same || n + 1 < a.F)
-                            prefetch<DM>(srcs(a, same ? ch + 1 : ch0, same ? n : n + 1), lane, pf);
-                    }
-                    wave_lds_sync();
-                    STAMP(1);
-                    int rtA, rtB;
-                    if (n == 0 || nospec) {   // rt_n is known
-                        rtA = rtB = sv_rt[n & 3][ci];
-                    } else {
-                        // mi_{n-1}: front(n-2)'s candidate selected by valid_{n-3}
-                        const int sel = sv_val[(n + 1) & 3][ci] ? 0 : 1;
-                        rtA = sv_mi[(n - 1) & 3][sel][ci] + QK_NPRE;
-                        rtB = sv_rt[(n - 1) & 3][ci];
-                    }
-                    const bool two = rtA != rtB;
-                    fir_dec(lane, rtA, M, dA);
-                    if (two) fir_dec(lane, rtB, M, dB);
-                    fir_head(lane, M, dA, two ? dB : nullptr);
-                    wave_lds_sync();
-                    STAMP(8);
-                    const int miA = hunt<MODE>(lane, M, dA, BT FACC_ARG);
-                    int miB = miA;
-                    if (two) {
-                        wave_lds_sync();
-                        miB = hunt<MODE>(lane, M, dB, BT FACC_ARG);
-                    }
-                    STAMP(9);
-                    if (lane == 0) {
-                        sv_mi[(n + 1) & 3][0][ci] = miA;
-                        sv_mi[(n + 1) & 3][1][ci] = miB;
-                    }
-                    store_window(lane, miA, dA, w0 + (size_t)ch * kWinStride);
-                    if (!nospec) store_window(lane, miB, two ? dB : dA, w1 + (size_t)ch * kWinStride);
-                    wave_lds_sync();
-                    STAMP(6);
-                }
-                signal_add(&fcnt[0][n & 1], 1, lane);
-                STAMP(5);
-            }
-            STAMP_FLUSH();
-            carry_history<DM>(a.in, a.hist, a.F, ch0, nlive, lane);
-        }
-        __syncthreads();
-        if (wave == 0 && lane < W) {   // state for the next call's first frame
-            const int ch = grp0 * W + lane;
-            if (ch < a.nch) {
-                const unsigned ge = a.g0 + (unsigned)a.F;
-                const int v2 = sv_val[(a.F + 2) & 3][lane], v1 = sv_val[(a.F + 3) & 3][lane];
-                mi_of(a, ge)[ch] = sv_mi[a.F & 3][(v2 || nospec) ? 0 : 1][lane];
-                rt_of(a, ge)[ch] = sv_rt[a.F & 3][lane];
-                a.vhist[ch] = (v2 ? 1 : 0) | (v1 ? 2 : 0);
-            }
-        }
-        return;
-    }
     if constexpr (DUAL) {
         // bseq[gi][p]: frames of parity p decided, summed over the chain's back
         // waves; frame m is decided by all of them once it reaches this
@@ -1636,8 +1461,7 @@ float bits2f(uint32_t u) {
 
 // rx_kernel instantiations (pick_shape below)
 struct Shape {
-    enum Kind { k4x2, k2x4d, k1x8d16, k1x8d32, k1x8d64, k1x8q16, k1x8q32, k1x8s16, k1x8s32,
-                k1x6i16, k1x6i32 };
+    enum Kind { k4x2, k2x4d, k1x8d16, k1x8d32, k1x8d64, k1x8q16, k1x8q32 };
     int kind;
     int roles;
 };
@@ -1686,10 +1510,6 @@ struct qpsk_ctx {
     int shape = -1;             // Shape::Kind forced by QPSK_SHAPE (A/B runs); -1: by batch size
     int width = 0;              // dual-chain group width forced by QPSK_WIDTH; 0: by batch size
     int quad = -1;              // quad-per-channel backs forced on/off by QPSK_QUAD; -1: by width
-    int spec = -1;              // speculative fronts forced on/off by QPSK_SPEC; -1: default
-    int iso = -1;               // back/front waves on separate SIMDs (QPSK_ISO); -1: default
-    float2* d_wspec = nullptr;  // SPEC windows [4][2][nslot][168] (contexts of <= 32 channels per CU)
-    int* d_vhist = nullptr;     // SPEC valid flags of the last two frames, [nslot]
     int prio = -1;              // issue priority forced by QPSK_PRIO (0 none, 1 front, 2 back)
     int* d_err = nullptr;       // device error word (kErrStall), cleared by qpsk_rx_sync
     hipStream_t last = nullptr; // stream of the latest qpsk_rx_batch_device call
@@ -1734,22 +1554,12 @@ static size_t nslot(const qpsk_ctx* c) {
     return (size_t)((c->ngroup + kMaxGroups - 1) / kMaxGroups) * kMaxGroups * QK_GROUP;
 }
 
-// the batch sizes whose default shape has quad backs (pick_shape): those
-// contexts also hold the speculative fronts' window planes (8 per channel)
-static bool spec_capable(const qpsk_ctx* c) {
-    return c->mode == QPSK_MODE_REFERENCE && (size_t)c->nch <= (size_t)32 * c->ncu;
-}
-
 static int ctx_alloc(qpsk_ctx* c) {
     HCHECK(hipMalloc(&c->d_ptab, sizeof(float2) * QK_FRAME));
     HCHECK(hipMalloc(&c->d_ks, sizeof(unsigned long long) * QK_KS_FRAMES));
     HCHECK(hipMalloc(&c->d_hist, sizeof(int16_t) * nslot(c) * 2 * QK_FRAME));
     HCHECK(hipMalloc(&c->d_njobs, sizeof(unsigned) * 2));
     HCHECK(hipMalloc(&c->d_err, sizeof(int)));
-    if (spec_capable(c)) {
-        HCHECK(hipMalloc(&c->d_wspec, sizeof(float2) * 8 * nslot(c) * kWinStride));
-        HCHECK(hipMalloc(&c->d_vhist, sizeof(int) * nslot(c)));
-    }
     for (int p = 0; p < 2; p++) {
         HCHECK(hipMalloc(&c->d_win[p], sizeof(float2) * nslot(c) * kWinStride));
         HCHECK(hipMalloc(&c->d_mi[p], sizeof(int) * nslot(c)));
@@ -1765,10 +1575,6 @@ extern "C" int qpsk_rx_reset(qpsk_ctx* c) {
     HCHECK(hipMemsetAsync(c->d_hist, 0, sizeof(int16_t) * ns * 2 * QK_FRAME, c->stream));
     HCHECK(hipMemsetAsync(c->d_njobs, 0, sizeof(unsigned) * 2, c->stream));
     HCHECK(hipMemsetAsync(c->d_err, 0, sizeof(int), c->stream));
-    if (c->d_wspec) {
-        HCHECK(hipMemsetAsync(c->d_wspec, 0, sizeof(float2) * 8 * ns * kWinStride, c->stream));
-        HCHECK(hipMemsetAsync(c->d_vhist, 0, sizeof(int) * ns, c->stream));
-    }
     for (int p = 0; p < 2; p++) {
         HCHECK(hipMemsetAsync(c->d_win[p], 0, sizeof(float2) * ns * kWinStride, c->stream));
         HCHECK(hipMemsetAsync(c->d_mi[p], 0, sizeof(int) * ns, c->stream));
@@ -1792,8 +1598,6 @@ static void ctx_free(qpsk_ctx* c) {
             if (c->ev[i][j]) (void)hipEventDestroy(c->ev[i][j]);
     (void)hipFree(c->d_ptab);
     (void)hipFree(c->d_err);
-    (void)hipFree(c->d_wspec);
-    (void)hipFree(c->d_vhist);
     (void)hipFree(c->d_jobs);
     (void)hipFree(c->d_njobs);
     (void)hipFree(c->d_ks);
@@ -1874,8 +1678,6 @@ extern "C" qpsk_ctx* qpsk_rx_create_mode(int device, int nch, int mode, int* err
         c->width = (v == 16 || v == 32 || v == 64) ? v : 0;
     }
     if (const char* qv = getenv("QPSK_QUAD")) c->quad = atoi(qv) != 0;
-    if (const char* sv = getenv("QPSK_SPEC")) c->spec = atoi(sv) != 0;
-    if (const char* iv = getenv("QPSK_ISO")) c->iso = atoi(iv) != 0;
     if (const char* pv = getenv("QPSK_PRIO"))
         c->prio = !strcmp(pv, "none") ? 0 : !strcmp(pv, "front") ? 1 : !strcmp(pv, "back") ? 2 : -1;
     if (const char* sh = getenv("QPSK_SHAPE")) {
@@ -1946,14 +1748,7 @@ static Shape pick_shape(const qpsk_ctx* c) {
         // waves per workgroup, whose 128-VGPR budget spills the front; the
         // lane-per-channel back stays there (profiles/r02_quad_ab.txt)
         const bool quad = W <= 32 && (c->quad >= 0 ? c->quad != 0 : true);
-        // the SPEC kernel (reference mode, window planes held): speculative
-        // fronts and/or isolated roles; without speculation it runs with kNoSpec
-        const bool spec = c->spec > 0, iso = c->iso > 0;
-        if (quad && c->d_wspec && (spec || iso)) {
-            sh.kind = iso ? (W == 16 ? Shape::k1x6i16 : Shape::k1x6i32)
-                          : (W == 16 ? Shape::k1x8s16 : Shape::k1x8s32);
-            if (!spec) sh.roles |= kNoSpec;
-        } else if (quad) {
+        if (quad) {
             sh.kind = W == 16 ? Shape::k1x8q16 : Shape::k1x8q32;
         } else {
             sh.kind = W == 16 ? Shape::k1x8d16 : W == 32 ? Shape::k1x8d32 : Shape::k1x8d64;
@@ -2003,40 +1798,26 @@ extern "C" int qpsk_rx_batch_device(qpsk_ctx* c, const int16_t* d_in, int F, uin
     }
     const int parity = (int)(c->calls & 1u);
     const Shape sh = pick_shape(c);
-#define QPSK_LAUNCH(GG, FF, MM, DD, WW, QQ, SS, II)                                            \
-    hipLaunchKernelGGL((rx_kernel<GG, FF, MM, DD, WW, QQ, SS, II>),                            \
+#define QPSK_LAUNCH(GG, FF, MM, DD, WW, QQ)                                                    \
+    hipLaunchKernelGGL((rx_kernel<GG, FF, MM, DD, WW, QQ>),                                    \
                        dim3((unsigned)((c->nch + (size_t)GG * WW - 1) / ((size_t)GG * WW))),   \
-                       dim3(64 * kBlockWavesOf<GG, FF, MM, DD, WW, QQ, II>), 0, s,             \
+                       dim3(64 * (kBackWavesOf<GG, FF, MM, DD, WW, QQ> + GG * FF)), 0, s,      \
                        d_in, c->d_hist, c->d_ptab,                                             \
                        c->d_ks, c->d_win[0], c->d_win[1], c->d_mi[0], c->d_mi[1], c->d_rt[0],  \
                        c->d_rt[1], d_bits, d_valid, d_trace, reinterpret_cast<float2*>(d_soft), \
                        c->d_jobs, c->d_njobs + parity, c->nch, F,                               \
                        (unsigned)(c->frames & 0xffffffffu), sh.roles, c->d_fft,                \
-                       (unsigned long long)c->jobs_cap, c->d_err, c->d_wspec,                  \
-                       (unsigned long long)(nslot(c) * kWinStride), c->d_vhist)
-// speculative fronts exist for the reference mode only (spec_capable)
-#define QPSK_LAUNCH_SPEC(MM, WW)                                                               \
-    do {                                                                                       \
-        if constexpr (MM == 0) QPSK_LAUNCH(1, 8, 0, true, WW, true, true, false);              \
-    } while (0)
-#define QPSK_LAUNCH_ISO(MM, WW)                                                                \
-    do {                                                                                       \
-        if constexpr (MM == 0) QPSK_LAUNCH(1, 6, 0, true, WW, true, true, true);               \
-    } while (0)
+                       (unsigned long long)c->jobs_cap, c->d_err)
 #define QPSK_LAUNCH_MODE(MM)                                                                   \
     do {                                                                                       \
         switch (sh.kind) {                                                                     \
-            case Shape::k2x4d: QPSK_LAUNCH(2, 4, MM, true, 64, false, false, false); break;           \
-            case Shape::k1x8d16: QPSK_LAUNCH(1, 8, MM, true, 16, false, false, false); break;         \
-            case Shape::k1x8d32: QPSK_LAUNCH(1, 8, MM, true, 32, false, false, false); break;         \
-            case Shape::k1x8d64: QPSK_LAUNCH(1, 8, MM, true, 64, false, false, false); break;         \
-            case Shape::k1x8q16: QPSK_LAUNCH(1, 8, MM, true, 16, true, false, false); break;          \
-            case Shape::k1x8q32: QPSK_LAUNCH(1, 8, MM, true, 32, true, false, false); break;          \
-            case Shape::k1x8s16: QPSK_LAUNCH_SPEC(MM, 16); break;                              \
-            case Shape::k1x8s32: QPSK_LAUNCH_SPEC(MM, 32); break;                              \
-            case Shape::k1x6i16: QPSK_LAUNCH_ISO(MM, 16); break;                               \
-            case Shape::k1x6i32: QPSK_LAUNCH_ISO(MM, 32); break;                               \
-            default: QPSK_LAUNCH(4, 2, MM, false, 64, false, false, false); break;                    \
+            case Shape::k2x4d: QPSK_LAUNCH(2, 4, MM, true, 64, false); break;                  \
+            case Shape::k1x8d16: QPSK_LAUNCH(1, 8, MM, true, 16, false); break;                \
+            case Shape::k1x8d32: QPSK_LAUNCH(1, 8, MM, true, 32, false); break;                \
+            case Shape::k1x8d64: QPSK_LAUNCH(1, 8, MM, true, 64, false); break;                \
+            case Shape::k1x8q16: QPSK_LAUNCH(1, 8, MM, true, 16, true); break;                 \
+            case Shape::k1x8q32: QPSK_LAUNCH(1, 8, MM, true, 32, true); break;                 \
+            default: QPSK_LAUNCH(4, 2, MM, false, 64, false); break;                           \
         }                                                                                      \
     } while (0)
     switch (c->mode) {
@@ -2046,8 +1827,6 @@ extern "C" int qpsk_rx_batch_device(qpsk_ctx* c, const int16_t* d_in, int F, uin
         default: QPSK_LAUNCH_MODE(3); break;
     }
 #undef QPSK_LAUNCH_MODE
-#undef QPSK_LAUNCH_SPEC
-#undef QPSK_LAUNCH_ISO
 #undef QPSK_LAUNCH
     HCHECK(hipGetLastError());
     if (slot >= 0) HCHECK(hipEventRecord(c->ev[slot][1], s));

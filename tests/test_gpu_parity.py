@@ -362,16 +362,12 @@ def test_random_batches_and_splits(seed):
     _assert_same(out, bits, valid, tr)
 
 
-@pytest.mark.parametrize("spec,iso", [("0", "0"), ("1", "0"), ("0", "1"), ("1", "1")])
 @pytest.mark.parametrize("nch", [100, 333, 8192])
-def test_speculative_fronts_on_and_off(nch, spec, iso, monkeypatch):
-    """Quad-back batches run speculative fronts by default (QPSK_SPEC=1): front(n)
-    computes D_n, the hunt and the window for both rx_timing candidates
-    (mi_{n-1} + 128 and rt_{n-1}, src/qpsk.c:219) and the back selects by
-    valid_{n-1}.  On and off, with calls of 1 frame and of odd lengths (the
-    selection state crosses call boundaries), every output equals the oracle."""
-    monkeypatch.setenv("QPSK_SPEC", spec)
-    monkeypatch.setenv("QPSK_ISO", iso)
+def test_quad_backs_across_call_splits(nch):
+    """Quad-back batches (<= 32 channels per CU) fed as calls of 1, 1, 4, 1 and
+    the remaining frames: the dual-chain state (both chains' rx_timing and
+    preamble positions, the frame parity of the windows) crosses every call
+    boundary, and every output equals the oracle."""
     nf = 13 if nch < 1000 else 9
     x = oracle.synth(140 + nch, nch, nf, 5.0 if nch != 333 else 1000.0)
     bits, valid, tr = oracle.cpu_rx(x, trace=True)
