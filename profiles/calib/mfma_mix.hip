@@ -12,6 +12,7 @@
 
 typedef float f2 __attribute__((ext_vector_type(2)));
 typedef float f4 __attribute__((ext_vector_type(4)));
+typedef float f16 __attribute__((ext_vector_type(16)));
 
 template <int OP, int PARTNER>
 __global__ void k(float* out, unsigned long long* cyc, int n) {
@@ -40,6 +41,7 @@ __global__ void k(float* out, unsigned long long* cyc, int n) {
         // partner: as many iterations as keep it busy for the VALU waves' whole run
         const float a = (float)threadIdx.x * 1e-3f, b = 1.0f;
         f4 acc0 = {0, 0, 0, 0}, acc1 = acc0, acc2 = acc0, acc3 = acc0;
+        f16 acc16 = {};
         f2 w = f2{a, 1.0f};
         const f2 d = f2{1e-7f, 2e-7f};
         const int m = n;
@@ -54,12 +56,19 @@ __global__ void k(float* out, unsigned long long* cyc, int n) {
                 acc2 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc2, 0, 0, 0);
                 acc3 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc3, 0, 0, 0);
             }
+            if (PARTNER == 4) {   // dependent 32x32x2 chain (2048 FMAs per MFMA)
+                acc16 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc16, 0, 0, 0);
+            }
+            if (PARTNER == 5) {   // dependent 4x4x1 (16 blocks) chain
+                acc0 = __builtin_amdgcn_mfma_f32_4x4x1f32(a, b, acc0, 0, 0, 0);
+                acc0 = __builtin_amdgcn_mfma_f32_4x4x1f32(a, b, acc0, 0, 0, 0);
+            }
             if (PARTNER == 3) {   // a packed-VALU partner of the same length
 #pragma unroll
                 for (int u = 0; u < 16; u++) asm volatile("v_pk_add_f32 %0, %0, %1" : "+v"(w) : "v"(d));
             }
         }
-        s = acc0[0] + acc1[1] + acc2[2] + acc3[3] + w.x;
+        s = acc0[0] + acc1[1] + acc2[2] + acc3[3] + w.x + acc16[5];
     }
     out[blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
@@ -87,6 +96,8 @@ int main() {
         run<0, 1>("v_pk_add_f32", "dependent mfma chain", out, cyc);
         run<0, 2>("v_pk_add_f32", "4 mfma chains", out, cyc);
         run<0, 3>("v_pk_add_f32", "pk_add stream", out, cyc);
+        run<0, 4>("v_pk_add_f32", "dep. 32x32x2 chain", out, cyc);
+        run<0, 5>("v_pk_add_f32", "dep. 4x4x1 chain", out, cyc);
         run<1, 0>("v_add_f32", "none", out, cyc);
         run<1, 1>("v_add_f32", "dependent mfma chain", out, cyc);
         run<1, 2>("v_add_f32", "4 mfma chains", out, cyc);
