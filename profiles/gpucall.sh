@@ -1,3 +1,3 @@
 set -o pipefail
-timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread -k "every_workgroup_shape" > gpurun_out/c8_pytest.log 2>&1 &&
-bash profiles/knob_ab.sh 3 65536 QPSK_SHAPE=4x2 QPSK_SHAPE=4x2l > gpurun_out/c8_ls_ab.txt 2>&1
+timeout -k 10 120 python -u profiles/stamps_lp.py 65536 > gpurun_out/c15_stamps_lp.txt 2>&1 &&
+timeout -k 10 120 python -u profiles/stamps_lp.py 16384 >> gpurun_out/c15_stamps_lp.txt 2>&1
