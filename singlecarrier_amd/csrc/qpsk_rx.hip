@@ -81,7 +81,7 @@ constexpr unsigned long long kPreLo = qhunt::pre_mask(0), kPreHi = qhunt::pre_ma
 
 struct RxArgs {
     const int16_t* in;       // [nch][F][1880]
-    int16_t* hist;           // [nch][3][1880]: frames -2, -1 of this call (row 2: rx_lp_kernel)
+    int16_t* hist;           // [nch][2][1880]: frames -2, -1 of this call
     const float2* ptab;      // [1880] mixer table P[t] * 2^-14
     const unsigned long long* ks;  // [1057] keystream bits of frame g (mod 1057)
     float2* win0;            // [nslot][168] equalizer windows, even global frames
@@ -168,7 +168,7 @@ __device__ __forceinline__ void signal_add(int* p, int v, int lane) {
 
 __device__ __forceinline__ const int16_t* frame_ptr(const RxArgs& a, int ch, int k) {
     return k >= 0 ? a.in + ((size_t)ch * a.F + k) * QK_FRAME
-                  : a.hist + ((size_t)ch * 3 + (k + 2)) * QK_FRAME;
+                  : a.hist + ((size_t)ch * 2 + (k + 2)) * QK_FRAME;
 }
 
 // ---------------------------------------------------------------- front wave
@@ -525,7 +525,7 @@ __device__ __forceinline__ void carry_history(const int16_t* in, int16_t* hist, 
     constexpr int kHead8 = MODE == 1 ? 213 : 149;
     for (int c = 0; c < nlive; c++) {
         const int ch = ch0 + c;
-        int16_t* h0 = hist + (size_t)ch * 3 * QK_FRAME;
+        int16_t* h0 = hist + (size_t)ch * 2 * QK_FRAME;
         int16_t* h1 = h0 + QK_FRAME;
         const int16_t* last = F >= 1 ? in + ((size_t)ch * F + (F - 1)) * QK_FRAME : h1;
         const int16_t* prev = F >= 2 ? in + ((size_t)ch * F + (F - 2)) * QK_FRAME : h1;
@@ -748,12 +748,7 @@ __device__ __forceinline__ Kal kal_reset() {
     return k;
 }
 
-// window slots 1..5 = dec[mi .. mi+4]; the unaligned form reads them one by one
-// (rx_lp_kernel's window is dec itself, at any mi)
-__device__ __forceinline__ void load_x0u(const f2* wp2, f2 (&x)[5]) {
-#pragma unroll
-    for (int t = 0; t < 5; t++) x[t] = wp2[1 + t];
-}
+// window slots 1..5 = dec[mi .. mi+4]
 __device__ __forceinline__ void load_x0(const float4* wp, f2 (&x)[5]) {
     const float4 w0 = ldw(wp + 0), w1 = ldw(wp + 1), w2 = ldw(wp + 2);
     x[0] = f2{w0.z, w0.w};
@@ -795,22 +790,20 @@ __device__ __forceinline__ int train(Kal& k, f2 (&x)[5], const f2* wp2, bool& ba
 // dec[mi .. mi+162]; read two slots (16 B) every two steps.
 // get_rt() yields rx_timing of frame n; it is called only after the training,
 // so the dual-chain kernel can wait for the previous frame's decision there.
-template <bool WIN_ALIGNED = true, typename RtFn>
+template <typename RtFn>
 __device__ __forceinline__ void back_frame(const RxArgs& a, int ch, bool live, int n, int mi,
                                            RtFn get_rt, const float2* win, int* rt_next) {
     const float4* wp = reinterpret_cast<const float4*>(win);
     Kal k = kal_reset();
     f2 x[5];
-    if constexpr (WIN_ALIGNED) load_x0(wp, x);
-    else load_x0u(reinterpret_cast<const f2*>(win), x);
+    load_x0(wp, x);
     // equalize(): 128 x train_eq (src/qpsk.c:111-123, src/equalizer.c:45-58)
     const f2* wp2 = reinterpret_cast<const f2*>(win);
     bool bad = (a.roles & kForceExact) != 0;
     int matches = train<false>(k, x, wp2, bad);
     if (__builtin_expect(__ballot(bad) != 0ull, 0)) {   // recompute the frame exactly
         k = kal_reset();
-        if constexpr (WIN_ALIGNED) load_x0(wp, x);
-        else load_x0u(reinterpret_cast<const f2*>(win), x);
+        load_x0(wp, x);
         matches = train<true>(k, x, wp2, bad);
     }
     const bool valid = live && matches > QK_MATCH_MIN;   // src/qpsk.c:196
@@ -1456,381 +1449,6 @@ __global__ void __launch_bounds__(64 * (kBackWavesOf<G, FP, MODE, DUAL, W, QUAD>
     }
 }
 
-// ---------------------------------------------------------------- lane-parallel front
-// rx_lp_kernel (DESIGN.md "Lane-parallel front"): the front of a group of 64
-// channels is ONE wave with a lane per channel, like the back.  Its RRC FIR is
-// a stream over the channel's samples with 10 running output sums (every
-// sample feeds ~10 decimated outputs), so the wave has ~20 independent packed
-// operations per sample instead of the LDS-fed output-parallel FIR's 3 chains.
-// The rx_timing offset differs per lane; the lane streams M[v + rt] for
-// v = 0, 1, ..., so the tap index of every running sum is the same in all lanes.
-// Its outputs dec_{n+1} = [D_n, F_{n+1}] go to HBM once (a [frame mod 3][ch]
-// row of kLpRow float2) and are read in place: by hunt waves (one channel at a
-// time, the MFMA correlator of qpsk_hunt.h) and by the back wave, whose window
-// is dec_row + mi - 1 (no window copy).
-//   per workgroup: 4 groups x (back wave, FIR wave, 2 hunt waves) = 16 waves
-//   iteration n:  back(n) trains frame n | FIR: D_n -> dec_{n+1}[0..187],
-//                 signal, then F_{n+2} -> dec_{n+2}[188..289] (rt-independent,
-//                 one frame ahead) | hunts: wait for D_n, mi_{n+1} per channel
-//   one __syncthreads() per frame.
-// Mixed samples m[u] = Q[u] * x[u] (src/qpsk.c:138-147): Q is the mixer table
-// over the M index u (u < 48: -P[1832 + u] of frame n-2, else P[u - 48] of
-// frame n-1; adjacent frames differ in sign), in two signs (frame parity).
-constexpr int kLpRow = 296;       // float2 per dec row (290 used, 16-B rows)
-constexpr int kLpQ = 1300;        // Q entries (u <= 999 + 255 + 46)
-constexpr int kLpHunt = 1;        // hunt waves per group
-constexpr int kLpWaves = 4 * (2 + kLpHunt);
-
-typedef int i4a __attribute__((ext_vector_type(4), aligned(4)));   // 4-B aligned 16-B load
-
-__device__ __forceinline__ i4a ldg4(const int* p) { return *reinterpret_cast<const i4a*>(p); }
-
-// The RRC taps are symmetric (h[k] == h[48-k], bitwise), so 25 values; they sit
-// in 13 VGPR pairs TP[j] = (h[2j], h[2j+1]) and a packed product picks one half
-// for both lanes by op_sel (a pk operand is a register pair; one tap per pair
-// would take 50 registers).
-constexpr bool rrc_symmetric() {
-    for (int k = 0; k < QK_NTAPS; k++)
-        if (QK_RRC[k] != QK_RRC[QK_NTAPS - 1 - k]) return false;
-    return true;
-}
-static_assert(rrc_symmetric(), "RRC taps are symmetric");
-constexpr int kTapPairs = 13;
-struct Taps { f2 p[kTapPairs]; };
-__device__ __forceinline__ Taps lp_taps() {
-    Taps t;
-#pragma unroll
-    for (int j = 0; j < kTapPairs; j++) t.p[j] = f2{QK_RRC[2 * j], 2 * j + 1 < 25 ? QK_RRC[2 * j + 1] : 0.0f};
-    return t;
-}
-// the two int16 samples 2k, 2k+1 of a stream that starts sh/16 samples into w[0]
-__device__ __forceinline__ int pair_at(int lo, int hi, int sh) {
-    return (int)__builtin_amdgcn_alignbit((unsigned)hi, (unsigned)lo, (unsigned)sh);
-}
-
-// compile-time loops (the FIR bodies must unroll completely: every tap and
-// accumulator index is then a constant and lives in a register)
-template <int N, typename Fn, int... I>
-__device__ __forceinline__ void sfor_impl(Fn&& fn, std::integer_sequence<int, I...>) {
-    (fn(std::integral_constant<int, I>{}), ...);
-}
-template <int N, typename Fn>
-__device__ __forceinline__ void sfor(Fn&& fn) {
-    sfor_impl<N>(fn, std::make_integer_sequence<int, N>{});
-}
-
-template <int K>
-__device__ __forceinline__ f2 tapmul(f2 m, const Taps& t) {
-    constexpr int d = K < QK_NTAPS - 1 - K ? K : QK_NTAPS - 1 - K;   // 0..24
-    f2 r;
-    if constexpr ((d & 1) == 0)
-        asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(r) : "v"(m), "v"(t.p[d >> 1]));
-    else
-        asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,1]" : "=v"(r) : "v"(m), "v"(t.p[d >> 1]));
-    return r;
-}
-
-__device__ __forceinline__ void ld7(const int* p, int (&A)[16], int (&B)[12], bool a, bool b) {
-    if (a) {
-        const i4a a0 = ldg4(p), a1 = ldg4(p + 4), a2 = ldg4(p + 8), a3 = ldg4(p + 12);
-        A[0] = a0.x; A[1] = a0.y; A[2] = a0.z; A[3] = a0.w; A[4] = a1.x; A[5] = a1.y; A[6] = a1.z; A[7] = a1.w;
-        A[8] = a2.x; A[9] = a2.y; A[10] = a2.z; A[11] = a2.w; A[12] = a3.x; A[13] = a3.y; A[14] = a3.z; A[15] = a3.w;
-    }
-    if (b) {
-        const i4a b0 = ldg4(p + 16), b1 = ldg4(p + 20), b2 = ldg4(p + 24);
-        B[0] = b0.x; B[1] = b0.y; B[2] = b0.z; B[3] = b0.w; B[4] = b1.x; B[5] = b1.y; B[6] = b1.z; B[7] = b1.w;
-        B[8] = b2.x; B[9] = b2.y; B[10] = b2.z; B[11] = b2.w;
-    }
-}
-
-// D_n of this lane's channel: D[i] = GAIN * sum_{k<49} h[k] M[5i + rt + k], i < 188
-// (src/fir.c:36-42, model-A decimation src/qpsk.c:157-162), streamed over
-// v = u - rt in blocks of 50 samples (10 outputs, so running sum i lives in
-// register slot i mod 10 at compile time).  m0: int16 M[0] of this channel
-// (frame n-2's sample 1832; M is contiguous), Q: LDS table of this frame's sign.
-// Samples arrive as 28 dwords per block (A: 16, B: 12); A is reloaded for the
-// next block once sample 29 is done, B after sample 49.
-__device__ __forceinline__ void lp_fir_dec(const int16_t* m0, int rt, const float2* Q, float2* out,
-                                           const Taps& tp) {
-    const int* w32 = reinterpret_cast<const int*>(m0) + (rt >> 1);   // block b: + 25 b dwords
-    const int sh = (rt & 1) * 16;
-    const float2* q = Q + rt;                                          // Q[v + rt]
-    f2 acc[10];
-    f2 hold = {0.0f, 0.0f};                                            // last even output
-    int A[16], B[12];
-    ld7(w32, A, B, true, true);
-    constexpr int kQA = 5;                          // mixer-table reads this many samples ahead (divides 50)
-    float2 qr[kQA];
-    sfor<kQA>([&](auto ic) { qr[decltype(ic)::value] = q[decltype(ic)::value]; });
-    for (int b = 0; b < 20; b++) {
-        const int* nx = w32 + 25 * (b + 1);
-        int w15 = 0;
-        sfor<50>([&](auto rc) {
-            constexpr int r = decltype(rc)::value;
-            // (the body of each sample is kept in place: a scheduler that hoists the
-            // block's loads and conversions spills hundreds of registers)
-            __builtin_amdgcn_sched_barrier(0);
-            constexpr int k2 = r >> 1;                  // sample pair
-            if constexpr (r == 30) {                    // A consumed: next block's A
-                w15 = A[15];
-                ld7(nx, A, B, true, false);
-            }
-            int lo, hi;
-            if constexpr (k2 < 15) lo = A[k2];
-            else if constexpr (k2 == 15) lo = w15;
-            else lo = B[k2 - 16];
-            if constexpr (k2 + 1 < 15) hi = A[k2 + 1];
-            else if constexpr (k2 + 1 == 15) hi = r < 30 ? A[15] : w15;
-            else hi = B[k2 - 15];
-            const int pr = pair_at(lo, hi, sh);
-            const float xf = (float)(int16_t)((r & 1) ? (pr >> 16) : (pr & 0xffff));
-            const float2 qv = qr[r % kQA];
-            qr[r % kQA] = q[50 * b + r + kQA];          // Q has kLpQ > 999 + 255 + kQA entries
-            const f2 m = f2{qv.x * xf, qv.y * xf};     // mixer, src/qpsk.c:143
-            sfor<19>([&](auto qc) {
-                constexpr int qq = decltype(qc)::value - 9;
-                constexpr int k = r - 5 * qq;
-                if constexpr (k >= 0 && k < QK_NTAPS) {
-                    constexpr int sl = (qq + 10) % 10;
-                    if constexpr (k == 0) acc[sl] = f2{0.0f, 0.0f} + tapmul<k>(m, tp);
-                    else acc[sl] = acc[sl] + tapmul<k>(m, tp);
-                    // the sum is formed here, not sunk to its store (that kept all 49
-                    // products of every running output live)
-                    asm volatile("" : "+v"(acc[sl]));
-                    if constexpr (k == QK_NTAPS - 1) {   // output i = 10 b + qq complete
-                        const int i = 10 * b + qq;
-                        const f2 o = acc[sl] * QK_GAIN;
-                        if constexpr ((qq & 1) == 0) {
-                            hold = o;
-                        } else {   // outputs outside 1..187 go to the unused entries 290-291
-                            float2* dst = (i >= 1 && i < QK_NDEC) ? out + (i - 1) : out + 290;
-                            *reinterpret_cast<float4*>(dst) = make_float4(hold.x, hold.y, o.x, o.y);
-                        }
-                    }
-                }
-            });
-            if constexpr (r == 49) ld7(nx, A, B, false, true);   // B consumed
-        });
-    }
-}
-
-// F_{n+1}[j] = GAIN * sum_k h[k] H[j + k], j < 102 (the undecimated head,
-// SURVEY.md A.6), H[s] = Q[s] x[s], s < 150, from h0 = frame n-1's sample 1832
-// (contiguous into frame n); six passes of 17 outputs over 65 samples each.
-__device__ __forceinline__ void lp_fir_head(const int16_t* h0, const float2* Q, float2* out, const Taps& tp) {
-    const int* w32 = reinterpret_cast<const int*>(h0);
-    for (int c = 0; c < 6; c++) {
-        const int s0 = 17 * c;
-        const int* p = w32 + (s0 >> 1);
-        const int sh = (s0 & 1) * 16;
-        int W[36];
-        sfor<9>([&](auto tc) {
-            constexpr int t = decltype(tc)::value;
-            const i4a v = ldg4(p + 4 * t);
-            W[4 * t] = v.x; W[4 * t + 1] = v.y; W[4 * t + 2] = v.z; W[4 * t + 3] = v.w;
-        });
-        f2 acc[17];
-        sfor<65>([&](auto rc) {
-            constexpr int r = decltype(rc)::value;
-            __builtin_amdgcn_sched_barrier(0);
-            const int pr = pair_at(W[r >> 1], W[(r >> 1) + 1], sh);
-            const float xf = (float)(int16_t)((r & 1) ? (pr >> 16) : (pr & 0xffff));
-            const float2 qv = Q[s0 + r];
-            const f2 m = f2{qv.x * xf, qv.y * xf};
-            sfor<17>([&](auto jc) {
-                constexpr int j = decltype(jc)::value;
-                constexpr int k = r - j;
-                if constexpr (k >= 0 && k < QK_NTAPS) {
-                    if constexpr (k == 0) acc[j] = f2{0.0f, 0.0f} + tapmul<k>(m, tp);
-                    else acc[j] = acc[j] + tapmul<k>(m, tp);
-                    asm volatile("" : "+v"(acc[j]));
-                    if constexpr (k == QK_NTAPS - 1) {
-                        const f2 o = acc[j] * QK_GAIN;
-                        out[QK_NDEC + s0 + j] = make_float2(o.x, o.y);
-                    }
-                }
-            });
-        });
-    }
-}
-
-// history rows of the lane-parallel front: [x_{-2}, x_{-1}, x_0 copy]; the copy
-// of x_0[0..kLpCopy) makes M of frame 1 (x_{-1}[1832..] ++ x_0) contiguous
-constexpr int kLpCopy = 1296;     // samples (> 1262, multiple of 8)
-
-__device__ __forceinline__ const int16_t* lp_frame(const RxArgs& a, int ch, int k) {
-    return k >= 0 ? a.in + ((size_t)ch * a.F + k) * QK_FRAME
-                  : a.hist + ((size_t)ch * 3 + (k + 2)) * QK_FRAME;
-}
-// M[0] of frame n (frame n-2's sample 1832) in contiguous memory
-__device__ __forceinline__ const int16_t* lp_m0(const RxArgs& a, int ch, int n) {
-    if (n == 1) return a.hist + ((size_t)ch * 3 + 1) * QK_FRAME + 1832;   // row 1 -> row 2
-    return lp_frame(a, ch, n - 2) + 1832;
-}
-
-__global__ void __launch_bounds__(64 * kLpWaves) rx_lp_kernel(
-    const int16_t* in, int16_t* hist, const float2* qtab, const unsigned long long* ks,
-    float2* dec, int* mi0, int* mi1, int* rt0, int* rt1, uint8_t* bits, uint8_t* valid,
-    int32_t* trace, float2* soft, float4* jobs, unsigned* njobs, int nch, int F, unsigned g0,
-    int g0mod3, int roles, unsigned long long jcap, unsigned long long dplane, int* err) {
-    const RxArgs a{in, hist, nullptr, ks, nullptr, nullptr, mi0, mi1, rt0, rt1, bits, valid, trace,
-                   soft, jobs, njobs, nch, F, g0, (size_t)jcap, roles, err};
-    constexpr int kG = 4;
-    __shared__ __attribute__((aligned(16))) float2 Qs[2][kLpQ];        // + / - sign
-    __shared__ __attribute__((aligned(16))) float BT[qhunt::kBT];
-    __shared__ __attribute__((aligned(16))) float2 HS[kG * kLpHunt][256];   // hunt: dec staging
-    __shared__ __attribute__((aligned(16))) float2 HT[kG * kLpHunt][qhunt::kTK / 2];   // TK image
-    __shared__ int mi_s[kG][2][QK_GROUP], rt_s[kG][2][QK_GROUP];
-    __shared__ int dsig[kG];
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int grp0 = blockIdx.x * kG;
-    for (int i = threadIdx.x; i < kLpQ; i += 64 * kLpWaves) {
-        const float2 v = qtab[i];
-        Qs[0][i] = v;
-        Qs[1][i] = make_float2(-v.x, -v.y);
-    }
-    qhunt::bconst_lds(threadIdx.x, 64 * kLpWaves, BT);
-    if (wave < kG) {   // every lane, dead ones too: mi and rt steer addresses here
-        const int ch = (grp0 + wave) * QK_GROUP + lane;
-        const bool in = ch < a.nch;
-        mi_s[wave][0][lane] = in ? mi_of(a, a.g0)[ch] : 0;
-        rt_s[wave][0][lane] = in ? rt_of(a, a.g0)[ch] : QK_RT0;
-        mi_s[wave][1][lane] = 0;
-        rt_s[wave][1][lane] = QK_RT0;
-    }
-    if (threadIdx.x < kG) dsig[threadIdx.x] = 0;
-    auto drow = [&](int n, int ch) {   // dec row of local frame n (global g0 + n)
-        return dec + (size_t)((g0mod3 + n) % 3) * dplane + (size_t)ch * kLpRow;
-    };
-    const int role = wave / kG, gi = wave % kG;   // 0 back, 1 FIR, 2.. hunt
-    const int gch0 = (grp0 + gi) * QK_GROUP;
-    if (role == 1) {
-        // prologue: copy x_0[0..kLpCopy) into history row 2 (cooperatively, channel by
-        // channel), then F_1 from x_{-1}[1832..] ++ x_0 (before the table barrier
-        // only the copy; F_1 needs Qs)
-        for (int c = 0; c < QK_GROUP && gch0 + c < a.nch; c++) {
-            const int4* s4 = reinterpret_cast<const int4*>(lp_frame(a, gch0 + c, 0));
-            int4* d4 = reinterpret_cast<int4*>(a.hist + ((size_t)(gch0 + c) * 3 + 2) * QK_FRAME);
-            for (int u = lane; u < kLpCopy / 8; u += 64) d4[u] = s4[u];
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
-    if (role == 0) {
-        // ------------------------------------------------------------ back
-        const int ch = gch0 + lane;
-        const bool live = ch < a.nch;
-        const bool any = gch0 < a.nch;
-        if (((a.roles >> 4) & 3) == 2) __builtin_amdgcn_s_setprio(2);
-        // diagnostic stamps (QPSK_STAMPS): 0 back work, 1 back at the barrier
-        STAMP_DECL
-        for (int n = 0; n < a.F; n++) {
-            const int p = n & 1;
-            if (any) {
-                const int rt = rt_s[gi][p][lane];
-                const int mi = live ? mi_s[gi][p][lane] & (QK_NLAG - 1) : 0;   // in [0, 128)
-                back_frame<false>(a, live ? ch : 0, live, n, mi, [=] { return rt; },
-                                  drow(n, live ? ch : 0) + mi - 1, &rt_s[gi][p ^ 1][lane]);
-            } else {
-                rt_s[gi][p ^ 1][lane] = rt_s[gi][p][lane];
-            }
-            STAMP(0);
-            __syncthreads();
-            STAMP(1);
-        }
-        STAMP_FLUSH();
-        if (live) {
-            const unsigned ge = a.g0 + (unsigned)a.F;
-            mi_of(a, ge)[ch] = mi_s[gi][a.F & 1][lane];
-            rt_of(a, ge)[ch] = rt_s[gi][a.F & 1][lane];
-        }
-    } else if (role == 1) {
-        // ------------------------------------------------------------ FIR
-        const int ch = gch0 + lane;
-        const bool live = ch < a.nch;
-        const int cs = live ? ch : 0;   // input of a dead lane: channel 0's; its outputs go to
-                                        // its own (unused, < nslot) dec row
-        const Taps tp = lp_taps();
-        if (((a.roles >> 4) & 3) == 1) __builtin_amdgcn_s_setprio(2);
-        // F_1: frames -1 and 0, sign of frame 0 (global g0)
-        lp_fir_head(a.hist + ((size_t)cs * 3 + 1) * QK_FRAME + 1832, Qs[a.g0 & 1u], drow(1, ch), tp);
-        // stamps: 2 D_n, 3 signal, 4 F_{n+2}, 5 FIR at the barrier
-        STAMP_DECL
-        for (int n = 0; n < a.F; n++) {
-            const int p = n & 1;
-            // D_n: M from frames n-2 (u < 48) and n-1, sign of frame n-1
-            // rt = mi + 128 or QK_RT0 < 256 (the mask only bounds the addresses)
-            lp_fir_dec(lp_m0(a, cs, n), live ? rt_s[gi][p][lane] & 255 : QK_RT0,
-                       Qs[(a.g0 + (unsigned)n - 1u) & 1u], drow(n + 1, ch), tp);
-            STAMP(2);
-            signal_add(&dsig[gi], 1, lane);
-            STAMP(3);
-            // F_{n+2}: frames n and n+1, sign of frame n+1 (one frame ahead)
-            if (n + 1 < a.F)
-                lp_fir_head(lp_frame(a, cs, n) + 1832, Qs[(a.g0 + (unsigned)n + 1u) & 1u],
-                            drow(n + 2, ch), tp);
-            STAMP(4);
-            __syncthreads();
-            STAMP(5);
-        }
-        STAMP_FLUSH();
-        // history for the next call: rows 0, 1 = x_{F-2}, x_{F-1} (row 2 is refilled)
-        for (int c = 0; c < QK_GROUP && gch0 + c < a.nch; c++) {
-            const int cc = gch0 + c;
-            int16_t* h0 = a.hist + (size_t)cc * 3 * QK_FRAME;
-            int16_t* h1 = h0 + QK_FRAME;
-            const int16_t* last = lp_frame(a, cc, a.F - 1);
-            const int16_t* prev = a.F >= 2 ? lp_frame(a, cc, a.F - 2) : h1;
-            if (lane < 6) {   // F == 1: prev is h1; its load completes before the h1 stores
-                const int t = 1832 + 8 * lane;
-                *reinterpret_cast<int4*>(h0 + t) = *reinterpret_cast<const int4*>(prev + t);
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            for (int u = lane; u < QK_FRAME / 8; u += 64)
-                reinterpret_cast<int4*>(h1)[u] = reinterpret_cast<const int4*>(last)[u];
-        }
-    } else {
-        // ------------------------------------------------------------ hunt
-        const int h = role - 2;                          // 0 .. kLpHunt-1
-        const int hw = gi * kLpHunt + h;
-        float2* S = HS[hw];
-        float2* T = HT[hw];
-        const int cb = h * (QK_GROUP / kLpHunt), ce = cb + QK_GROUP / kLpHunt;
-        const int cend = min(ce, a.nch - gch0);
-        // stamps: 6 wait for D_n, 7 hunts, 8 hunt wave at the barrier
-        STAMP_DECL
-        for (int n = 0; n < a.F; n++) {
-            const int p = n & 1;
-            spin_wait(&dsig[gi], n + 1, a.err);
-            STAMP(6);
-            float4 d0 = {}, d1 = {};
-            if (cb < cend) {
-                const float4* r = reinterpret_cast<const float4*>(drow(n + 1, gch0 + cb));
-                d0 = r[lane];
-                d1 = r[64 + lane];
-            }
-            for (int c = cb; c < cend; c++) {
-                reinterpret_cast<float4*>(S)[lane] = d0;
-                reinterpret_cast<float4*>(S)[64 + lane] = d1;
-                if (c + 1 < cend) {   // next channel's dec row
-                    const float4* r = reinterpret_cast<const float4*>(drow(n + 1, gch0 + c + 1));
-                    d0 = r[lane];
-                    d1 = r[64 + lane];
-                }
-                wave_lds_sync();
-                const int mi = hunt<0>(lane, T, S, BT FACC_ARG);
-                if (lane == 0) mi_s[gi][p ^ 1][c] = mi;
-                wave_lds_sync();
-            }
-            STAMP(7);
-            __syncthreads();
-            STAMP(8);
-        }
-        STAMP_FLUSH();
-    }
-}
-
 // ---------------------------------------------------------------- host side
 
 float bits2f(uint32_t u) {
@@ -1843,7 +1461,7 @@ float bits2f(uint32_t u) {
 
 // rx_kernel instantiations (pick_shape below)
 struct Shape {
-    enum Kind { k4x2, k2x4d, k1x8d16, k1x8d32, k1x8d64, k1x8q16, k1x8q32, kLp };
+    enum Kind { k4x2, k2x4d, k1x8d16, k1x8d32, k1x8d64, k1x8q16, k1x8q32 };
     int kind;
     int roles;
 };
@@ -1862,8 +1480,6 @@ struct qpsk_ctx {
     float2* d_ptab = nullptr;
     unsigned long long* d_ks = nullptr;
     int16_t* d_hist = nullptr;
-    float2* d_dec = nullptr;    // rx_lp_kernel: [3][nslot][kLpRow] dec rows
-    float2* d_qtab = nullptr;   // rx_lp_kernel: mixer table Q over the M index
     float2* d_win[2] = {nullptr, nullptr};
     int* d_mi[2] = {nullptr, nullptr};
     int* d_rt[2] = {nullptr, nullptr};
@@ -1941,11 +1557,7 @@ static size_t nslot(const qpsk_ctx* c) {
 static int ctx_alloc(qpsk_ctx* c) {
     HCHECK(hipMalloc(&c->d_ptab, sizeof(float2) * QK_FRAME));
     HCHECK(hipMalloc(&c->d_ks, sizeof(unsigned long long) * QK_KS_FRAMES));
-    HCHECK(hipMalloc(&c->d_hist, sizeof(int16_t) * nslot(c) * 3 * QK_FRAME));
-    if (c->mode == QPSK_MODE_REFERENCE) {   // rx_lp_kernel: dec rows by frame mod 3, mixer table Q
-        HCHECK(hipMalloc(&c->d_dec, sizeof(float2) * 3 * nslot(c) * kLpRow));
-        HCHECK(hipMalloc(&c->d_qtab, sizeof(float2) * kLpQ));
-    }
+    HCHECK(hipMalloc(&c->d_hist, sizeof(int16_t) * nslot(c) * 2 * QK_FRAME));
     HCHECK(hipMalloc(&c->d_njobs, sizeof(unsigned) * 2));
     HCHECK(hipMalloc(&c->d_err, sizeof(int)));
     for (int p = 0; p < 2; p++) {
@@ -1960,8 +1572,7 @@ extern "C" int qpsk_rx_reset(qpsk_ctx* c) {
     if (!c) return QPSK_EINVAL;
     HCHECK(hipSetDevice(c->device));
     const size_t ns = nslot(c);
-    HCHECK(hipMemsetAsync(c->d_hist, 0, sizeof(int16_t) * ns * 3 * QK_FRAME, c->stream));
-    if (c->d_dec) HCHECK(hipMemsetAsync(c->d_dec, 0, sizeof(float2) * 3 * ns * kLpRow, c->stream));
+    HCHECK(hipMemsetAsync(c->d_hist, 0, sizeof(int16_t) * ns * 2 * QK_FRAME, c->stream));
     HCHECK(hipMemsetAsync(c->d_njobs, 0, sizeof(unsigned) * 2, c->stream));
     HCHECK(hipMemsetAsync(c->d_err, 0, sizeof(int), c->stream));
     for (int p = 0; p < 2; p++) {
@@ -1991,8 +1602,6 @@ static void ctx_free(qpsk_ctx* c) {
     (void)hipFree(c->d_njobs);
     (void)hipFree(c->d_ks);
     (void)hipFree(c->d_hist);
-    (void)hipFree(c->d_dec);
-    (void)hipFree(c->d_qtab);
     (void)hipFree(c->d_fft);
     for (int p = 0; p < 2; p++) {
         (void)hipFree(c->d_win[p]);
@@ -2072,8 +1681,7 @@ extern "C" qpsk_ctx* qpsk_rx_create_mode(int device, int nch, int mode, int* err
     if (const char* pv = getenv("QPSK_PRIO"))
         c->prio = !strcmp(pv, "none") ? 0 : !strcmp(pv, "front") ? 1 : !strcmp(pv, "back") ? 2 : -1;
     if (const char* sh = getenv("QPSK_SHAPE")) {
-        c->shape = !strcmp(sh, "4x2") ? Shape::k4x2 : !strcmp(sh, "lp") ? Shape::kLp
-                 : !strcmp(sh, "2x4d") ? Shape::k2x4d
+        c->shape = !strcmp(sh, "4x2") ? Shape::k4x2 : !strcmp(sh, "2x4d") ? Shape::k2x4d
                  : !strcmp(sh, "1x8") ? Shape::k1x8d64 : -1;
     }
     int r = herr(hipSetDevice(device));
@@ -2090,12 +1698,6 @@ extern "C" qpsk_ctx* qpsk_rx_create_mode(int device, int nch, int mode, int* err
         static unsigned long long ksf[QK_KS_FRAMES];
         build_tables(ptab, ksf);
         r = herr(hipMemcpy(c->d_ptab, ptab, sizeof ptab, hipMemcpyHostToDevice));
-        if (r == QPSK_OK && c->d_qtab) {   // Q[u] = u < 48 ? -P[1832 + u] : P[u - 48]
-            static float2 q[kLpQ];
-            for (int u = 0; u < kLpQ; u++)
-                q[u] = u < 48 ? make_float2(-ptab[1832 + u].x, -ptab[1832 + u].y) : ptab[u - 48];
-            r = herr(hipMemcpy(c->d_qtab, q, sizeof q, hipMemcpyHostToDevice));
-        }
         if (r == QPSK_OK) r = herr(hipMemcpy(c->d_ks, ksf, sizeof ksf, hipMemcpyHostToDevice));
     }
     if (r == QPSK_OK && (mode & QPSK_MODE_FFT_HUNT)) r = fft_hunt_tables(c);
@@ -2218,15 +1820,7 @@ extern "C" int qpsk_rx_batch_device(qpsk_ctx* c, const int16_t* d_in, int F, uin
             default: QPSK_LAUNCH(4, 2, MM, false, 64, false); break;                           \
         }                                                                                      \
     } while (0)
-    if (sh.kind == Shape::kLp && c->d_dec) {
-        hipLaunchKernelGGL(rx_lp_kernel, dim3((unsigned)((c->nch + 255) / 256)), dim3(64 * kLpWaves), 0, s,
-                           d_in, c->d_hist, c->d_qtab, c->d_ks, c->d_dec, c->d_mi[0], c->d_mi[1],
-                           c->d_rt[0], c->d_rt[1], d_bits, d_valid, d_trace,
-                           reinterpret_cast<float2*>(d_soft), c->d_jobs, c->d_njobs + parity, c->nch, F,
-                           (unsigned)(c->frames & 0xffffffffu), (int)(c->frames % 3), sh.roles,
-                           (unsigned long long)c->jobs_cap, (unsigned long long)(nslot(c) * kLpRow),
-                           c->d_err);
-    } else switch (c->mode) {
+    switch (c->mode) {
         case 0: QPSK_LAUNCH_MODE(0); break;
         case 1: QPSK_LAUNCH_MODE(1); break;
         case 2: QPSK_LAUNCH_MODE(2); break;
