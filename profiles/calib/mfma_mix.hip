@@ -45,6 +45,7 @@ __global__ void k(float* out, unsigned long long* cyc, int n) {
         f2 w = f2{a, 1.0f};
         const f2 d = f2{1e-7f, 2e-7f};
         const int m = n;
+        const unsigned long long t0 = __builtin_amdgcn_s_memtime();
         for (int i = 0; i < m; i++) {
             if (PARTNER == 1) {   // dependent chain (the hunt)
                 acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc0, 0, 0, 0);
@@ -69,6 +70,8 @@ __global__ void k(float* out, unsigned long long* cyc, int n) {
             }
         }
         s = acc0[0] + acc1[1] + acc2[2] + acc3[3] + w.x + acc16[5];
+        const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+        if ((threadIdx.x & 63) == 0) atomicAdd(cyc + 1, t1 - t0);
     }
     out[blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
@@ -76,21 +79,24 @@ __global__ void k(float* out, unsigned long long* cyc, int n) {
 template <int OP, int PARTNER>
 void run(const char* name, const char* partner, float* out, unsigned long long* cyc) {
     const int n = 8192;
-    (void)hipMemset(cyc, 0, 8);
+    (void)hipMemset(cyc, 0, 16);
     const int waves = PARTNER ? 8 : 4;
     hipLaunchKernelGGL((k<OP, PARTNER>), dim3(256), dim3(64 * waves), 0, 0, out, cyc, n);
     (void)hipDeviceSynchronize();
-    unsigned long long c;
-    (void)hipMemcpy(&c, cyc, 8, hipMemcpyDeviceToHost);
-    const double per_wave = (double)c / (256.0 * 4);
-    printf("%-13s 8 chains, partner %-22s cycles/instr = %.2f\n", name, partner, per_wave / (n * 8.0));
+    unsigned long long c[2];
+    (void)hipMemcpy(c, cyc, 16, hipMemcpyDeviceToHost);
+    const double per_wave = (double)c[0] / (256.0 * 4);
+    const double pw = (double)c[1] / (256.0 * 4);
+    const double nm = PARTNER == 1 || PARTNER == 5 ? 2.0 * n : PARTNER == 2 ? 4.0 * n : PARTNER == 4 ? 1.0 * n : 16.0 * n;
+    printf("%-13s 8 chains, partner %-22s cycles/instr = %.2f   partner: %.0f cycles, %.1f per instr\n", name,
+           partner, per_wave / (n * 8.0), pw, PARTNER ? pw / nm : 0.0);
 }
 
 int main() {
     float* out;
     unsigned long long* cyc;
     (void)hipMalloc(&out, 256 * 512 * sizeof(float));
-    (void)hipMalloc(&cyc, 8);
+    (void)hipMalloc(&cyc, 16);
     for (int rep = 0; rep < 2; rep++) {
         run<0, 0>("v_pk_add_f32", "none", out, cyc);
         run<0, 1>("v_pk_add_f32", "dependent mfma chain", out, cyc);
