@@ -1,2 +1,2 @@
 set -o pipefail
-timeout -k 10 120 ./profiles/calib/mfma_mix > gpurun_out/mfma_mix3.txt 2>&1
+timeout -k 10 900 python -u bench.py --sweep > gpurun_out/c19_sweep.jsonl 2> gpurun_out/c19_sweep.err
