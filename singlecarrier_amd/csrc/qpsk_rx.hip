@@ -604,8 +604,8 @@ __host__ __device__ constexpr int uix(int i, int j) { return j * (j - 1) / 2 + i
 // recomputes the whole frame with EXACT = true (IEEE division).  No branch in
 // the step, so the step is one basic block.
 // the gain half of update_eq: kalman_calculate (src/kalman.c:85-141); returns
-// kalman_y (the last 6.22 y).  It never reads eq or the error, so the gain
-// recursion of a frame depends only on its window (rx_kernel<.., ESPLIT>).
+// kalman_y (the last 6.22 y).  It never reads eq or the error: the gain
+// recursion of a frame depends only on its window.
 template <bool EXACT>
 __device__ __forceinline__ float kal_gain(Kal& k, const f2 (&x)[5], bool& bad) {
     const float E = QK_KAL_E, q = QK_KAL_Q;
@@ -797,108 +797,13 @@ __device__ __forceinline__ int train(Kal& k, f2 (&x)[5], const f2* wp2, bool& ba
     return matches;
 }
 
-
-// ---------------------------------------------------------------- split back
-// rx_kernel<.., ES> (1 group of 64 channels, lane backs): the gain recursion
-// of a frame (kalman_calculate, ~190 of the step's ~234 instructions) does not
-// depend on the error or eq, so it runs alone on the chain's back wave ("G"),
-// and an error wave ("E", lane = the same channel) runs val / error / eq
-// update / matches (src/equalizer.c:25-58) a few steps behind it from the
-// gains G hands over through an LDS ring (g[0..4] and kalman_y per step and
-// lane).  At the end of the frame E hands eq and matches back.  Every fp32
-// operation is update_eq()'s, on the same operands in the same order.  The
-// exact-division retrain (never taken in practice) runs the whole step on G.
-constexpr int kESR = 4;          // ring steps
-constexpr int kESFrame = 130;    // counter values per frame: 128 steps, the hand-back
-struct EsLink {
-    float4* ring;                // [kESR][3][64] (this chain)
-    int* gprog;                  // steps written by G (all frames of the call: base + step + 1)
-    int* eprog;                  // steps read by E; base + 129 once eq / matches are handed back
-    int base;                    // this frame's counter base
-};
-
-__device__ __forceinline__ int lds_ld(int* p) {
-    return __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-}
-__device__ __forceinline__ void lds_wait(int* p, int v, int* err) {
-    unsigned it = 0;
-    for (; it < kSpinBound && lds_ld(p) < v; it++) __builtin_amdgcn_s_sleep(1);
-    if (it == kSpinBound && __lane_id() == 0) atomicOr(err, kErrStall);
-}
-
-// G: 128 gain steps; step i's g[0..4] and y go to ring slot i mod kESR
-__device__ __forceinline__ void train_gain(Kal& k, f2 (&x)[5], const f2* wp2, bool& bad,
-                                           const EsLink& es, int lane, int* err) {
-#pragma unroll 4
-    for (int i = 0; i < QK_NPRE; i++) {
-        const f2 nx = wp2[i + 6];
-        const int ep = lds_ld(es.eprog);             // read early; checked before the ring write
-        const float y = kal_gain<false>(k, x, bad);
-        if (i >= kESR && ep < es.base + i - kESR + 1) lds_wait(es.eprog, es.base + i - kESR + 1, err);
-        float4* r = es.ring + (i % kESR) * 3 * 64 + lane;
-        r[0] = make_float4(k.g[0].x, k.g[0].y, k.g[1].x, k.g[1].y);
-        r[64] = make_float4(k.g[2].x, k.g[2].y, k.g[3].x, k.g[3].y);
-        r[128] = make_float4(k.g[4].x, k.g[4].y, y, 0.0f);
-        // LDS operations of a wave complete in order: the step is in the ring
-        // before the counter moves (all lanes store the same value)
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        __hip_atomic_store(es.gprog, es.base + i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#pragma unroll
-        for (int t = 0; t < 4; t++) x[t] = x[t + 1];
-        x[4] = nx;
-    }
-}
-
-// E: the error half of 128 train_eq steps (src/equalizer.c:45-58), then eq and
-// matches into ring slot (127 mod kESR)
-__device__ __forceinline__ void e_frame(const float2* win, const EsLink& es, int lane, int* err) {
-    const f2* wp2 = reinterpret_cast<const f2*>(win);
-    lds_wait(es.gprog, es.base + 1, err);            // G started: the window is complete
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    f2 x[5], eq[5];
-    load_x0(reinterpret_cast<const float4*>(win), x);
-#pragma unroll
-    for (int t = 0; t < 5; t++) eq[t] = f2{0.0f, 0.0f};
-    int matches = 0;
-#pragma unroll 4
-    for (int i = 0; i < QK_NPRE; i++) {
-        const f2 nx = wp2[i + 6];
-        const unsigned long long m = i < 64 ? kPreLo : kPreHi;
-        const float ref = ((m >> (i & 63)) & 1ull) ? 1.0f : -1.0f;
-        f2 v = {0.0f, 0.0f};
-#pragma unroll
-        for (int t = 0; t < 5; t++) v = v + cmul(x[t], eq[t]);
-        const float er = ref - v.x;                  // conjf(ref - val) = (ref - vr, vi)
-        if (lds_ld(es.gprog) < es.base + i + 1) lds_wait(es.gprog, es.base + i + 1, err);
-        const float4* r = es.ring + (i % kESR) * 3 * 64 + lane;
-        const float4 r0 = r[0], r1 = r[64], r2 = r[128];
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        __hip_atomic_store(es.eprog, es.base + i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        const f2 g[5] = {{r0.x, r0.y}, {r0.z, r0.w}, {r1.x, r1.y}, {r1.z, r1.w}, {r2.x, r2.y}};
-        const f2 e = f2{er, v.y} * r2.z;             // error *= kalman_y
-#pragma unroll
-        for (int t = 0; t < 5; t++) eq[t] = eq[t] + cmulc(e, g[t]);
-        if (er * ref > 0.0f) matches++;
-#pragma unroll
-        for (int t = 0; t < 4; t++) x[t] = x[t + 1];
-        x[4] = nx;
-    }
-    float4* r = es.ring + ((QK_NPRE - 1) % kESR) * 3 * 64 + lane;
-    r[0] = make_float4(eq[0].x, eq[0].y, eq[1].x, eq[1].y);
-    r[64] = make_float4(eq[2].x, eq[2].y, eq[3].x, eq[3].y);
-    r[128] = make_float4(eq[4].x, eq[4].y, __int_as_float(matches), 0.0f);
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    __hip_atomic_store(es.eprog, es.base + kESFrame - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
 // One frame of the back wave: lane = channel.  Window slots 1..163 hold
 // dec[mi .. mi+162]; read two slots (16 B) every two steps.
 // get_rt() yields rx_timing of frame n; it is called only after the training,
 // so the dual-chain kernel can wait for the previous frame's decision there.
-template <bool ES = false, typename RtFn>
+template <typename RtFn>
 __device__ __forceinline__ void back_frame(const RxArgs& a, int ch, bool live, int n, int mi,
-                                           RtFn get_rt, const float2* win, int* rt_next,
-                                           const EsLink* es = nullptr) {
+                                           RtFn get_rt, const float2* win, int* rt_next) {
     const float4* wp = reinterpret_cast<const float4*>(win);
     Kal k = kal_reset();
     f2 x[5];
@@ -906,19 +811,7 @@ __device__ __forceinline__ void back_frame(const RxArgs& a, int ch, bool live, i
     // equalize(): 128 x train_eq (src/qpsk.c:111-123, src/equalizer.c:45-58)
     const f2* wp2 = reinterpret_cast<const f2*>(win);
     bool bad = (a.roles & kForceExact) != 0;
-    int matches;
-    if constexpr (ES) {   // gains here, the error half on the E wave
-        train_gain(k, x, wp2, bad, *es, lane_id(), a.err);
-        lds_wait(es->eprog, es->base + kESFrame - 1, a.err);
-        const float4* r = es->ring + ((QK_NPRE - 1) % kESR) * 3 * 64 + lane_id();
-        const float4 r0 = r[0], r1 = r[64], r2 = r[128];
-        k.eq[0] = f2{r0.x, r0.y}; k.eq[1] = f2{r0.z, r0.w};
-        k.eq[2] = f2{r1.x, r1.y}; k.eq[3] = f2{r1.z, r1.w};
-        k.eq[4] = f2{r2.x, r2.y};
-        matches = __float_as_int(r2.z);
-    } else {
-        matches = train<false>(k, x, wp2, bad);
-    }
+    int matches = train<false>(k, x, wp2, bad);
     if (__builtin_expect(__ballot(bad) != 0ull, 0)) {   // recompute the frame exactly
         k = kal_reset();
         load_x0(wp, x);
@@ -1328,42 +1221,31 @@ __global__ void __launch_bounds__(256) rx_data_kernel(const float4* jobs, unsign
 template <int G, int FP, int MODE, bool DUAL, int W, bool QUAD>
 constexpr int kBackWavesOf = DUAL ? 2 * G * (QUAD ? W / 16 : 1) : G;
 
-// ES (DUAL, one group of 64, lane backs, reference mode): two error waves,
-// one per frame chain, beside the back waves (split back, above).
-template <int G, int FP, int MODE, bool DUAL, int W, bool QUAD, bool ES>
-constexpr int kBlockWavesOf = kBackWavesOf<G, FP, MODE, DUAL, W, QUAD> + (ES ? 2 : 0) + G * FP;
-
-template <int G, int FP, int MODE, bool DUAL, int W = QK_GROUP, bool QUAD = false, bool ES = false>
-__global__ void __launch_bounds__(64 * (kBlockWavesOf<G, FP, MODE, DUAL, W, QUAD, ES>), 3) rx_kernel(
+template <int G, int FP, int MODE, bool DUAL, int W = QK_GROUP, bool QUAD = false>
+__global__ void __launch_bounds__(64 * (kBackWavesOf<G, FP, MODE, DUAL, W, QUAD> + G * FP), 3) rx_kernel(
     const int16_t* in, int16_t* hist, const float2* ptab, const unsigned long long* ks,
     float2* win0, float2* win1, int* mi0, int* mi1, int* rt0, int* rt1, uint8_t* bits,
     uint8_t* valid, int32_t* trace, float2* soft, float4* jobs, unsigned* njobs, int nch, int F,
     unsigned g0, int roles, const float* fft_tab, unsigned long long jcap, int* err) {
     static_assert(W == QK_GROUP || (DUAL && G == 1 && W % FP == 0 && W <= QK_GROUP), "group width");
     static_assert(!QUAD || (DUAL && G == 1 && W % 16 == 0), "quad backs: dual chain, one group");
-    static_assert(!ES || (DUAL && G == 1 && W == QK_GROUP && !QUAD && MODE == 0), "split backs");
     constexpr int kGroups = G, kFrontPer = FP;
     constexpr int kBackWaves = kBackWavesOf<G, FP, MODE, DUAL, W, QUAD>;
     constexpr int kChainWaves = QUAD ? W / 16 : 1;     // back waves per frame chain and group
     constexpr int kFrontCh = W / kFrontPer;            // channels per front wave
     constexpr int kFrontWaves = kGroups * kFrontPer;
-    constexpr int kExtra = ES ? 2 : 0;                 // error waves
-    constexpr int kFirstFront = kBackWaves + kExtra;
-    constexpr int kBlock = 64 * kBlockWavesOf<G, FP, MODE, DUAL, W, QUAD, ES>;
+    constexpr int kBlock = 64 * (kBackWaves + kFrontWaves);
     const RxArgs a{in, hist, ptab, ks, win0, win1, mi0, mi1, rt0, rt1, bits, valid, trace, soft,
                    jobs, njobs, nch, F, g0, (size_t)jcap, roles, err};
     __shared__ __attribute__((aligned(16))) float2 P[QK_FRAME];
     constexpr int DM = MODE & 1;   // decimation semantics; MODE & 2: FFT hunt
-    // ES keeps one dec buffer per front wave (as MODE 1): LDS for the ring
-    constexpr int kM = Cfg<DM>::kM, kDecBuf = ES ? 1 : Cfg<DM>::kDecBuf;
+    constexpr int kM = Cfg<DM>::kM, kDecBuf = Cfg<DM>::kDecBuf;
     __shared__ __attribute__((aligned(16))) float2 Ms[kFrontWaves][kM];
     __shared__ __attribute__((aligned(16))) float2 decs[kFrontWaves][kDecBuf][kDec];
     __shared__ int mi_s[kGroups][2][QK_GROUP], rt_s[kGroups][2][QK_GROUP];
     // hunt tables: the MFMA correlator's B, or the FFT hunt's twiddles / Q / permutation
     __shared__ __attribute__((aligned(16))) float BT[(MODE & 2) ? kFftHT : qhunt::kBT];
     __shared__ int bseq[kGroups][2], fcnt[kGroups][2];   // DUAL progress counters, per group
-    __shared__ float4 es_ring[ES ? 2 : 1][ES ? kESR * 3 * 64 : 1];   // ES: per chain
-    __shared__ int es_prog[2][2];                               // ES: [chain][gprog, eprog]
     const int lane = threadIdx.x & 63;
     // wave-uniform by construction; readfirstlane tells the compiler, so every
     // per-wave index and pointer below lives in SGPRs
@@ -1384,7 +1266,6 @@ __global__ void __launch_bounds__(64 * (kBlockWavesOf<G, FP, MODE, DUAL, W, QUAD
         }
     }
     if (threadIdx.x < 2 * kGroups) (&bseq[0][0])[threadIdx.x] = (&fcnt[0][0])[threadIdx.x] = 0;
-    if (threadIdx.x < 4) (&es_prog[0][0])[threadIdx.x] = 0;
     __syncthreads();
     if constexpr (DUAL) {
         // bseq[gi][p]: frames of parity p decided, summed over the chain's back
@@ -1419,32 +1300,17 @@ __global__ void __launch_bounds__(64 * (kBlockWavesOf<G, FP, MODE, DUAL, W, QUAD
                     return rt_s[gi][p][idx];
                 };
                 const float2* wn = win_of(a, a.g0 + (unsigned)n) + (size_t)(live ? ch : 0) * kWinStride;
-                if constexpr (QUAD) {
+                if constexpr (QUAD)
                     back_frame_quad(a, live ? ch : 0, live, n, mi, get_rt, wn, &rt_s[gi][p ^ 1][idx]);
-                } else if constexpr (ES) {
-                    const EsLink es{es_ring[wave & 1], &es_prog[wave & 1][0], &es_prog[wave & 1][1],
-                                    (n >> 1) * kESFrame};
-                    back_frame<true>(a, live ? ch : 0, live, n, mi, get_rt, wn, &rt_s[gi][p ^ 1][idx], &es);
-                } else {
+                else
                     back_frame(a, live ? ch : 0, live, n, mi, get_rt, wn, &rt_s[gi][p ^ 1][idx]);
-                }
                 signal_add(&bseq[gi][p], 1, lane);
                 STAMP(13);
             }
             STAMP_FLUSH();
-        } else if (ES && wave < kFirstFront) {
-            // ---------------------------------------------------- error waves (ES)
-            const int chain = wave - kBackWaves;
-            const int ch = grp0 * W + lane;
-            __builtin_amdgcn_s_setprio(2);
-            for (int n = chain; n < a.F; n += 2) {
-                const EsLink es{es_ring[chain], &es_prog[chain][0], &es_prog[chain][1], (n >> 1) * kESFrame};
-                e_frame(win_of(a, a.g0 + (unsigned)n) + (size_t)(ch < a.nch ? ch : 0) * kWinStride, es,
-                        lane, a.err);
-            }
         } else {
             // ---------------------------------------------------- front
-            const int f = wave - kFirstFront;
+            const int f = wave - kBackWaves;
             const int gi = f / kFrontPer;
             const int fl = f % kFrontPer;
             // roles bits 16-19 (split s, one group per workgroup only; pick_shape
@@ -1452,7 +1318,7 @@ __global__ void __launch_bounds__(64 * (kBlockWavesOf<G, FP, MODE, DUAL, W, QUAD
             // wave (waves 4, 5, 8, 9 when waves map to SIMDs by wave % 4) take s
             // channels fewer, the others s more
             const int split = kGroups == 1 ? (a.roles >> 16) & 15 : 0;
-            auto share = [&](int x) { return ((x + kFirstFront) & 3) < kBackWaves; };
+            auto share = [&](int x) { return ((x + kBackWaves) & 3) < kBackWaves; };
             int cbeg = 0;
             for (int x = 0; x < fl; x++) cbeg += kFrontCh + (share(x) ? -split : split);
             const int mych = kFrontCh + (share(fl) ? -split : split);
@@ -1606,7 +1472,7 @@ float bits2f(uint32_t u) {
 
 // rx_kernel instantiations (pick_shape below)
 struct Shape {
-    enum Kind { k4x2, k2x4d, k1x8d16, k1x8d32, k1x8d64, k1x8q16, k1x8q32, k1x8e64 };
+    enum Kind { k4x2, k2x4d, k1x8d16, k1x8d32, k1x8d64, k1x8q16, k1x8q32 };
     int kind;
     int roles;
 };
@@ -1655,7 +1521,6 @@ struct qpsk_ctx {
     int shape = -1;             // Shape::Kind forced by QPSK_SHAPE (A/B runs); -1: by batch size
     int width = 0;              // dual-chain group width forced by QPSK_WIDTH; 0: by batch size
     int quad = -1;              // quad-per-channel backs forced on/off by QPSK_QUAD; -1: by width
-    int esplit = -1;            // split (gain / error) lane backs at W = 64 forced by QPSK_ESPLIT
     int prio = -1;              // issue priority forced by QPSK_PRIO (0 none, 1 front, 2 back)
     int* d_err = nullptr;       // device error word (kErrStall), cleared by qpsk_rx_sync
     hipStream_t last = nullptr; // stream of the latest qpsk_rx_batch_device call
@@ -1824,7 +1689,6 @@ extern "C" qpsk_ctx* qpsk_rx_create_mode(int device, int nch, int mode, int* err
         c->width = (v == 16 || v == 32 || v == 64) ? v : 0;
     }
     if (const char* qv = getenv("QPSK_QUAD")) c->quad = atoi(qv) != 0;
-    if (const char* ev = getenv("QPSK_ESPLIT")) c->esplit = atoi(ev) != 0;
     if (const char* pv = getenv("QPSK_PRIO"))
         c->prio = !strcmp(pv, "none") ? 0 : !strcmp(pv, "front") ? 1 : !strcmp(pv, "back") ? 2 : -1;
     if (const char* sh = getenv("QPSK_SHAPE")) {
@@ -1900,7 +1764,6 @@ static Shape pick_shape(const qpsk_ctx* c) {
         } else {
             sh.kind = W == 16 ? Shape::k1x8d16 : W == 32 ? Shape::k1x8d32 : Shape::k1x8d64;
             if (W == 64) sh.roles = (sh.roles & ~((3 << 4) | (15 << 16))) | (2 << 4) | (2 << 16);
-            if (W == 64 && c->mode == QPSK_MODE_REFERENCE && c->esplit > 0) sh.kind = Shape::k1x8e64;
         }
     }
     if (c->prio >= 0) sh.roles = (sh.roles & ~(3 << 4)) | (c->prio << 4);
@@ -1946,32 +1809,26 @@ extern "C" int qpsk_rx_batch_device(qpsk_ctx* c, const int16_t* d_in, int F, uin
     }
     const int parity = (int)(c->calls & 1u);
     const Shape sh = pick_shape(c);
-#define QPSK_LAUNCH(GG, FF, MM, DD, WW, QQ, EE)                                                \
-    hipLaunchKernelGGL((rx_kernel<GG, FF, MM, DD, WW, QQ, EE>),                                \
+#define QPSK_LAUNCH(GG, FF, MM, DD, WW, QQ)                                                    \
+    hipLaunchKernelGGL((rx_kernel<GG, FF, MM, DD, WW, QQ>),                                    \
                        dim3((unsigned)((c->nch + (size_t)GG * WW - 1) / ((size_t)GG * WW))),   \
-                       dim3(64 * kBlockWavesOf<GG, FF, MM, DD, WW, QQ, EE>), 0, s,             \
+                       dim3(64 * (kBackWavesOf<GG, FF, MM, DD, WW, QQ> + GG * FF)), 0, s,      \
                        d_in, c->d_hist, c->d_ptab,                                             \
                        c->d_ks, c->d_win[0], c->d_win[1], c->d_mi[0], c->d_mi[1], c->d_rt[0],  \
                        c->d_rt[1], d_bits, d_valid, d_trace, reinterpret_cast<float2*>(d_soft), \
                        c->d_jobs, c->d_njobs + parity, c->nch, F,                               \
                        (unsigned)(c->frames & 0xffffffffu), sh.roles, c->d_fft,                \
                        (unsigned long long)c->jobs_cap, c->d_err)
-// split backs exist for the reference mode (pick_shape selects them only there)
-#define QPSK_LAUNCH_ES(MM)                                                                     \
-    do {                                                                                       \
-        if constexpr (MM == 0) QPSK_LAUNCH(1, 8, 0, true, 64, false, true);                    \
-    } while (0)
 #define QPSK_LAUNCH_MODE(MM)                                                                   \
     do {                                                                                       \
         switch (sh.kind) {                                                                     \
-            case Shape::k2x4d: QPSK_LAUNCH(2, 4, MM, true, 64, false, false); break;                  \
-            case Shape::k1x8d16: QPSK_LAUNCH(1, 8, MM, true, 16, false, false); break;                \
-            case Shape::k1x8d32: QPSK_LAUNCH(1, 8, MM, true, 32, false, false); break;                \
-            case Shape::k1x8d64: QPSK_LAUNCH(1, 8, MM, true, 64, false, false); break;                \
-            case Shape::k1x8q16: QPSK_LAUNCH(1, 8, MM, true, 16, true, false); break;                 \
-            case Shape::k1x8q32: QPSK_LAUNCH(1, 8, MM, true, 32, true, false); break;                 \
-            case Shape::k1x8e64: QPSK_LAUNCH_ES(MM); break;                                     \
-            default: QPSK_LAUNCH(4, 2, MM, false, 64, false, false); break;                           \
+            case Shape::k2x4d: QPSK_LAUNCH(2, 4, MM, true, 64, false); break;                  \
+            case Shape::k1x8d16: QPSK_LAUNCH(1, 8, MM, true, 16, false); break;                \
+            case Shape::k1x8d32: QPSK_LAUNCH(1, 8, MM, true, 32, false); break;                \
+            case Shape::k1x8d64: QPSK_LAUNCH(1, 8, MM, true, 64, false); break;                \
+            case Shape::k1x8q16: QPSK_LAUNCH(1, 8, MM, true, 16, true); break;                 \
+            case Shape::k1x8q32: QPSK_LAUNCH(1, 8, MM, true, 32, true); break;                 \
+            default: QPSK_LAUNCH(4, 2, MM, false, 64, false); break;                           \
         }                                                                                      \
     } while (0)
     switch (c->mode) {
@@ -1981,7 +1838,6 @@ extern "C" int qpsk_rx_batch_device(qpsk_ctx* c, const int16_t* d_in, int F, uin
         default: QPSK_LAUNCH_MODE(3); break;
     }
 #undef QPSK_LAUNCH_MODE
-#undef QPSK_LAUNCH_ES
 #undef QPSK_LAUNCH
     HCHECK(hipGetLastError());
     if (slot >= 0) HCHECK(hipEventRecord(c->ev[slot][1], s));
