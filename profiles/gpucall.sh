@@ -1,4 +1,4 @@
 set -o pipefail
-QPSK_ESPLIT=1 QPSK_WIDTH=64 timeout -k 10 120 python -u profiles/lp_check.py > gpurun_out/c20_es_check.txt 2>&1 &&
-QPSK_ESPLIT=1 QPSK_WIDTH=64 QPSK_FORCE_EXACT=1 timeout -k 10 120 python -u profiles/lp_check.py >> gpurun_out/c20_es_check.txt 2>&1 &&
-bash profiles/knob_ab.sh 2 16384 QPSK_ESPLIT=0 QPSK_ESPLIT=1 > gpurun_out/c20_es_ab.txt 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r02_pytest_gpu_v5.log 2>&1 &&
+timeout -k 10 300 python -u bench.py > gpurun_out/r02_bench_v5.json 2> gpurun_out/r02_bench_v5.err &&
+bash profiles/profile.sh r02_v5 > gpurun_out/r02_v5_profile.log 2>&1
