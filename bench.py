@@ -67,6 +67,23 @@ def reduce_step(dist, wall: float, nch: int):
     return float(tmax.item()), int(tot.item())
 
 
+def init_host_group(rank: int, world: int):
+    """The ranks' host-side gloo group (barrier and time reduction only).
+    gloo's native code announces its peer connections on fd 1; the driver
+    reads rank 0's stdout as the one JSON line, so fd 1 points at stderr
+    while the group forms."""
+    import torch.distributed as dist
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    finally:
+        os.dup2(saved, 1)
+        os.close(saved)
+    return dist
+
+
 def free_port() -> int:
     import socket
     s = socket.socket()
@@ -335,12 +352,15 @@ def main():
     if world > 1:
         # host-side group: the timing barrier and the reductions only (the
         # data path has no collective)
-        import torch.distributed as dist
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dist = init_host_group(rank, world)
 
     import torch
     import singlecarrier_amd as sc
 
+    # one GPU per rank; ranks beyond the visible devices share them (only a
+    # launcher rehearsal on a one-GPU box does that: its timing means nothing)
+    ndev = torch.cuda.device_count()
+    local = local % ndev if ndev > 0 else local
     torch.cuda.set_device(local)
     nch, c0 = shard(args.channels, world, rank, strong)
     nf = args.frames
@@ -535,6 +555,8 @@ def main():
             "verified_vs_oracle": all(v is not None and v["ok"] for v in per_rank) if args.verify else None,
             "verified_per_rank": per_rank if args.verify else None,
             "stream_pcie": stream,
+            "gpus_visible": ndev,
+            "shared_gpus": world > ndev,   # a launcher rehearsal: not a scaling figure
         }
         print(json.dumps(out), flush=True)
     if dist:

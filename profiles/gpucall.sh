@@ -1,4 +1,6 @@
 set -o pipefail
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r02_pytest_gpu_v5.log 2>&1 &&
-timeout -k 10 300 python -u bench.py > gpurun_out/r02_bench_v5.json 2> gpurun_out/r02_bench_v5.err &&
-bash profiles/profile.sh r02_v5 > gpurun_out/r02_v5_profile.log 2>&1
+# launcher rehearsal on a one-GPU box: two ranks share the GPU (timing is not a
+# scaling figure; the check is the spawn, the gloo reduction and per-rank parity)
+B="--steps 3 --warmup 1 --cpu-channels 256 --cpu-all-channels 0 --stream-chunks 0"
+timeout -k 10 300 python -u bench.py --gpus 2 $B > gpurun_out/r02_launch_n2.json 2> gpurun_out/r02_launch_n2.err &&
+timeout -k 10 300 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 $B > gpurun_out/r02_torchrun_n2.json 2> gpurun_out/r02_torchrun_n2.err

@@ -34,12 +34,11 @@ def test_shard_weak():
 WORKER = textwrap.dedent('''
     import json, os, sys
     sys.path.insert(0, {root!r})
-    import torch.distributed as dist
     import bench
     import singlecarrier_amd as sc
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     assert os.environ["MASTER_ADDR"] == "127.0.0.1" and int(os.environ["LOCAL_RANK"]) == rank
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist = bench.init_host_group(rank, world)
     nch, c0 = bench.shard(1000, world, rank)
     # a rank's synthetic shard = the same channels of the whole batch (c0 offset)
     x = sc.synth(5, nch, 2, c0=c0)
@@ -53,15 +52,18 @@ WORKER = textwrap.dedent('''
 ''')
 
 
-def test_launcher_two_rank_gloo_sharding_and_reduction(tmp_path):
+def test_launcher_two_rank_gloo_sharding_and_reduction(tmp_path, capfd):
     """bench.launch() is what `python bench.py --gpus 2` runs without torchrun:
     two child processes with RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set, gloo on
-    127.0.0.1, MAX of times and SUM of channels on every rank."""
+    127.0.0.1, MAX of times and SUM of channels on every rank.  The group's
+    setup writes nothing to stdout (rank 0's stdout is the bench's one JSON
+    line)."""
     if not os.path.exists(os.path.join(ROOT, "singlecarrier_amd", "libqpsk_hip.so")):
         pytest.skip("library not built")
     script = tmp_path / "worker.py"
     script.write_text(WORKER.format(root=ROOT, out=str(tmp_path)))
     assert bench.launch(2, [], script=str(script)) == 0
+    assert capfd.readouterr().out == ""
     res = [json.load(open(tmp_path / f"r{r}.json")) for r in range(2)]
     (r0, n0, c00, t0, tot0, s0, g0), (r1, n1, c01, t1, tot1, s1, g1) = res
     assert (n0, n1, c00, c01) == (500, 500, 0, 500)
