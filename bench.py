@@ -135,8 +135,8 @@ def cpu_info() -> dict:
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--channels", type=int, default=65536,
                     help="channels of the batch (split over the GPUs; per GPU with --weak)")
     ap.add_argument("--frames", type=int, default=32)
@@ -405,9 +405,12 @@ def main():
         rx.demod_device(x, bits, valid)
     ev1.record()
     torch.cuda.synchronize()
+    # this rank's time ends when its GPU is done; the closing barrier stays
+    # outside it (a gloo round trip is ~0.1-1 ms, a step at N = 8 ~1.5 ms),
+    # and the MAX over ranks below is the slowest GPU
+    wall = time.perf_counter() - t0
     if dist:
         dist.barrier()
-    wall = time.perf_counter() - t0
     rx.sync()   # a device-side failure of any timed call raises here
     rx_ms, data_ms, kern_frames = rx.collect_timing_split()
     kern_ms = rx_ms + data_ms

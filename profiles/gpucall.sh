@@ -1,6 +1,5 @@
 set -o pipefail
-# launcher rehearsal on a one-GPU box: two ranks share the GPU (timing is not a
-# scaling figure; the check is the spawn, the gloo reduction and per-rank parity)
-B="--steps 3 --warmup 1 --cpu-channels 256 --cpu-all-channels 0 --stream-chunks 0"
-timeout -k 10 300 python -u bench.py --gpus 2 $B > gpurun_out/r02_launch_n2.json 2> gpurun_out/r02_launch_n2.err &&
-timeout -k 10 300 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 $B > gpurun_out/r02_torchrun_n2.json 2> gpurun_out/r02_torchrun_n2.err
+# default bench line (N = 1), then the N = 2 launcher rehearsal (two ranks on
+# the one GPU: not a scaling figure)
+timeout -k 10 400 python -u bench.py > gpurun_out/r02_bench_v6.json 2> gpurun_out/r02_bench_v6.err &&
+timeout -k 10 300 python -u bench.py --gpus 2 --cpu-channels 256 --cpu-all-channels 0 --stream-chunks 0 > gpurun_out/r02_launch_n2.json 2> gpurun_out/r02_launch_n2.err
