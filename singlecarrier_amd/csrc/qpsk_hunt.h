@@ -220,4 +220,180 @@ __device__ __forceinline__ f4 correlate_valu(int lane, const float2* TV) {
 __device__ __forceinline__ int lag_lo_valu(int lane) { return 2 * lane; }
 __device__ __forceinline__ int lag_hi_valu(int lane) { return 2 * lane + 1; }
 
+// ------------------------------------------------------- filtered hunt
+// The hunt needs only max_index (src/qpsk.c:172-183; max_value reaches no
+// output), so the exact sums are needed only when the argmax is in doubt.
+// First pass: the same 16x16 product with T split into two bf16 parts,
+// T = hi + lo + r (hi = RN_bf16(T), lo = RN_bf16(T - hi), |r| <= 2^-16 |T|),
+// on v_mfma_f32_16x16x32_bf16 (B = p or 0 is exact in bf16): 10 MFMAs of 16
+// cycles that hold the VALU for 8 each, against 36 f32 MFMAs that hold it for
+// ~29 each (profiles/calib/mfma_mix_r02.txt).  Per lag and component the
+// result S' is within
+//     d = 2^-13 W + 2^-100,   W = sum_{j<255} |Tr_j| + |Ti_j|
+// of the reference's sequential fp32 sum S: |S - sum T| <= 127u W (u = 2^-24)
+// for the reference's rounding, 2^-16 W for the split, at most 2u per
+// addition over the 160 terms of a chain in any order for the MFMA's fp32
+// accumulation (2^-15.7 W), u |S'| for the final hi + lo add, and 2^-126 per
+// term should the hardware flush bf16 denormals: 2^-14.6 W in all, 3x below d.
+// Hence cnormf(S) (src/qpsk.c:75-80, three roundings) lies in
+//     [L, U] = [(max(|Sr'|-d,0)^2 + max(|Si'|-d,0)^2)(1 - 2^-18),
+//               ((|Sr'|+d)^2 + (|Si'|+d)^2)(1 + 2^-18)]
+// (the factors also cover the roundings of computing L and U).  If exactly
+// one lag l* has U >= Lmax = max L, and Lmax > 0, then cnormf(S[l*]) is the
+// strict maximum and positive, so the reference's scan picks l*.  Otherwise
+// (ties, near-ties, an all-zero window) the caller runs the exact chain.
+typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
+constexpr int kHSteps = 5;                     // K = 160 = 5 x 32
+constexpr int kBH = kHSteps * 64 * 4;          // floats: B table, 16 B per lane and step (5 KB)
+constexpr int kPL = 176;                       // floats: p_q at [q + 16], q in [-16, 160), for the exact chain
+// bf16 images of T in the front's scratch (bytes): hi_r, hi_i, lo_r, lo_i, 272
+// entries each (255.. zero).  An imaginary image sits 16 B (mod 256) after its
+// real one, so the 16 lanes of each ds_read_b128 group cover the 64 banks once.
+__host__ __device__ constexpr int himg(int c) { return c == 0 ? 0 : c == 1 ? 784 : c == 2 ? 1536 : 2320; }
+constexpr int kHBytes = 2864;
+
+// B tables (once per workgroup): BH[s][lane] = p_{32s + 8(l>>4) + jj - (l&15)} or
+// 0, jj < 8, as bf16; PL for correlate_pl
+__device__ __forceinline__ void bconst_h_lds(int tid, int nthreads, float* BH) {
+    for (int x = tid; x < kHSteps * 64; x += nthreads) {
+        const int s = x >> 6, l = x & 63;
+        unsigned w[4];
+#pragma unroll
+        for (int jj = 0; jj < 8; jj += 2) {
+            unsigned v = 0;
+#pragma unroll
+            for (int e = 0; e < 2; e++) {
+                const int i = 32 * s + 8 * (l >> 4) + jj + e - (l & 15);
+                const unsigned b = (i >= 0 && i < QK_NPRE) ? (QK_PRE[i] > 0 ? 0x3F80u : 0xBF80u) : 0u;
+                v |= b << (16 * e);
+            }
+            w[jj >> 1] = v;
+        }
+        reinterpret_cast<uint4*>(BH)[x] = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    float* PL = BH + kBH;
+    for (int x = tid; x < kPL; x += nthreads) {
+        const int q = x - 16;
+        PL[x] = (q >= 0 && q < QK_NPRE) ? (float)QK_PRE[q] : 0.0f;
+    }
+}
+
+// sum over the wave (DPP row shifts / broadcasts); order-free: only a bound
+template <int CTRL, int RM, int BM>
+__device__ __forceinline__ float dpp_f32(float x) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, RM, BM, false));
+}
+__device__ __forceinline__ float wave_sum_f32(float v) {
+    v = v + dpp_f32<0x111, 0xf, 0xf>(v);   // row_shr:1
+    v = v + dpp_f32<0x112, 0xf, 0xf>(v);   // row_shr:2
+    v = v + dpp_f32<0x114, 0xf, 0xe>(v);   // row_shr:4
+    v = v + dpp_f32<0x118, 0xf, 0xc>(v);   // row_shr:8
+    v = v + dpp_f32<0x142, 0xa, 0xf>(v);   // row_bcast:15
+    v = v + dpp_f32<0x143, 0xc, 0xf>(v);   // row_bcast:31
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+
+// bf16 images of T (as store_t: T[j] = (RN(dr - di), RN(di + dr)), j < 255);
+// lane l writes j = 4l .. 4l+3 of each image.  Returns W (wave-uniform).
+__device__ __forceinline__ float store_h(int lane, const float2* dec, char* H) {
+    const float4* d4 = reinterpret_cast<const float4*>(dec + 4 * lane);
+    const float4 p = d4[0], q = d4[1];
+    const float dr[4] = {p.x, p.z, q.x, q.z}, di[4] = {p.y, p.w, q.y, q.w};
+    float t[2][4];   // [comp][r]
+    float w = 0.0f;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const bool in = 4 * lane + r < 2 * QK_NLAG - 1;
+        t[0][r] = in ? dr[r] - di[r] : 0.0f;
+        t[1][r] = in ? di[r] + dr[r] : 0.0f;
+        w = w + (__builtin_fabsf(t[0][r]) + __builtin_fabsf(t[1][r]));
+    }
+#pragma unroll
+    for (int c = 0; c < 2; c++) {
+        bf2 h[2], l[2];
+#pragma unroll
+        for (int e = 0; e < 2; e++) {
+            h[e] = bf2{(__bf16)t[c][2 * e], (__bf16)t[c][2 * e + 1]};   // RN
+            const float r0 = t[c][2 * e] - (float)h[e][0];               // exact
+            const float r1 = t[c][2 * e + 1] - (float)h[e][1];
+            l[e] = bf2{(__bf16)r0, (__bf16)r1};
+        }
+        uint2 hv, lv;
+        __builtin_memcpy(&hv, h, 8);
+        __builtin_memcpy(&lv, l, 8);
+        *reinterpret_cast<uint2*>(H + himg(c) + 8 * lane) = hv;
+        *reinterpret_cast<uint2*>(H + himg(2 + c) + 8 * lane) = lv;
+    }
+    if (lane < 2) {   // entries 256..271 (B = 0 there, but A must be finite)
+#pragma unroll
+        for (int c = 0; c < 4; c++)
+            *reinterpret_cast<uint4*>(H + himg(c) + 512 + 16 * lane) = make_uint4(0u, 0u, 0u, 0u);
+    }
+    return wave_sum_f32(w);
+}
+
+// The bf16 pass: this lane's D fragment (lags lag_lo / lag_hi, as correlate)
+__device__ __forceinline__ f4 correlate_h(int lane, const char* H, const float* BH) {
+    const int m = lane & 15, h = lane >> 4;
+    const int a = m >> 1, comp = m & 1;
+    const char* ahi = H + (comp ? himg(1) : himg(0)) + 32 * a + 16 * h;
+    const char* alo = H + (comp ? himg(3) : himg(2)) + 32 * a + 16 * h;
+    const bf8* bsrc = reinterpret_cast<const bf8*>(BH) + lane;
+    f4 acc_h = {0.0f, 0.0f, 0.0f, 0.0f}, acc_l = acc_h;
+#pragma unroll
+    for (int s = 0; s < kHSteps; s++) {
+        const bf8 b = bsrc[64 * s];
+        const bf8 xh = *reinterpret_cast<const bf8*>(ahi + 64 * s);
+        const bf8 xl = *reinterpret_cast<const bf8*>(alo + 64 * s);
+        acc_h = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xh, b, acc_h, 0, 0, 0);
+        acc_l = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xl, b, acc_l, 0, 0, 0);
+    }
+    return acc_h + acc_l;
+}
+
+__device__ __forceinline__ void cn_bounds(float sr, float si, float d, float& U, float& L) {
+    const float ar = __builtin_fabsf(sr), ai = __builtin_fabsf(si);
+    const float ur = ar + d, ui = ai + d;
+    const float lr = __builtin_fmaxf(ar - d, 0.0f), li = __builtin_fmaxf(ai - d, 0.0f);
+    U = (ur * ur + ui * ui) * (1.0f + 0x1p-18f);
+    L = (lr * lr + li * li) * (1.0f - 0x1p-18f);
+}
+
+// max_index from the bf16 pass when it is certain (see above), else -1.
+// `W` is store_h's bound sum; wave_max is the caller's u32 wave max.
+template <typename WaveMax>
+__device__ __forceinline__ int pick_h(int lane, f4 s, float W, WaveMax wave_max) {
+    const float d = W * 0x1p-13f + 0x1p-100f;
+    float U0, L0, U1, L1;
+    cn_bounds(s[0], s[1], d, U0, L0);
+    cn_bounds(s[2], s[3], d, U1, L1);
+    // L >= 0: its bits order as unsigned; NaN cannot occur (T is finite)
+    const unsigned lm = wave_max(max(__float_as_uint(L0), __float_as_uint(L1)));
+    if (lm == 0u) return -1;
+    const float Lm = __uint_as_float(lm);
+    const unsigned long long b0 = __ballot(U0 >= Lm), b1 = __ballot(U1 >= Lm);
+    if (__popcll(b0) + __popcll(b1) != 1) return -1;
+    return b0 ? lag_lo(__ffsll((long long)b0) - 1) : lag_hi(__ffsll((long long)b1) - 1);
+}
+
+// The exact chain (correlate) with B from the PL line: step s of lane l uses
+// p_{4s + (l>>4) - (l&15)} = PL[16 + 4s + (l>>4) - (l&15)].
+__device__ __forceinline__ f4 correlate_pl(int lane, const float* TK, const float* PL) {
+    const int m = lane & 15, kk = lane >> 4;
+    const int a = m >> 1, comp = m & 1;
+    const f4* src = reinterpret_cast<const f4*>(TK + (kk * 2 + comp) * kRow + 4 * a);
+    const float* bl = PL + 16 + kk - m;   // m == n == lane & 15
+    f4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int t = 0; t < kSteps / 4; t++) {
+        const f4 v = src[t];
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(v.x, bl[16 * t + 0], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(v.y, bl[16 * t + 4], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(v.z, bl[16 * t + 8], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(v.w, bl[16 * t + 12], acc, 0, 0, 0);
+    }
+    return acc;
+}
+
 }  // namespace qhunt

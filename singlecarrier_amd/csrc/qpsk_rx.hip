@@ -66,6 +66,9 @@ constexpr int kDec = 296;
 #ifndef QPSK_HUNT_MFMA
 #define QPSK_HUNT_MFMA 1   // 1: hunt on the matrix cores; 0: packed VALU chains (A/B knob)
 #endif
+#ifndef QPSK_HUNT_FILTER
+#define QPSK_HUNT_FILTER 1   // 1: bf16 first pass, exact chain only when the argmax is in doubt (qpsk_hunt.h)
+#endif
 
 constexpr int kM1 = 1240;
 template <int MODE> struct Cfg;
@@ -341,6 +344,9 @@ __device__ __forceinline__ void fir_dec752(int lane, int rt, const float2* M, fl
 // inverse [256, 512), Q [512, 768) as (re, im) pairs, then kf_work's input
 // permutation as 256 ints.
 constexpr int kFftHT = 768 * 2 + 256;   // floats
+// hunt tables (floats): the bf16 pass's B table + the exact chain's p line, or
+// the exact chain's B table
+constexpr int kHuntTab = QPSK_HUNT_FILTER ? qhunt::kBH + qhunt::kPL : qhunt::kBT;
 __device__ __forceinline__ int fft_hunt(int lane, float2* M, const float2* dec, const float* HT) {
     const qfft::cf* tw = reinterpret_cast<const qfft::cf*>(HT);
     const int* perm = reinterpret_cast<const int*>(HT + 768 * 2);
@@ -442,11 +448,25 @@ __device__ __forceinline__ int hunt(int lane, float2* M, const float2* dec, cons
     if constexpr ((MODE & 2) != 0) return fft_hunt(lane, M, dec, BT);
 #if QPSK_HUNT_MFMA
     // on the matrix cores (qpsk_hunt.h: bit-identical k-ordered chain)
+#if QPSK_HUNT_FILTER
+    {   // bf16 pass; certain argmax -> done
+        char* H = reinterpret_cast<char*>(M);
+        const float W = qhunt::store_h(lane, dec, H);
+        wave_lds_sync();
+        const int pick = qhunt::pick_h(lane, qhunt::correlate_h(lane, H, BT), W, wave_max_u32);
+        if (pick >= 0) return pick;
+        wave_lds_sync();   // the exact image below overwrites H
+    }
+#endif
     float* TK = reinterpret_cast<float*>(M);
     qhunt::store_t(lane, dec, TK);
     wave_lds_sync();
     FSTAMP(2);
+#if QPSK_HUNT_FILTER
+    const qhunt::f4 acc = qhunt::correlate_pl(lane, TK, BT + qhunt::kBH);
+#else
     const qhunt::f4 acc = qhunt::correlate_bt(lane, TK, BT);
+#endif
     FSTAMP(3);
 #define QPSK_LAG_LO qhunt::lag_lo
 #define QPSK_LAG_HI qhunt::lag_hi
@@ -1244,7 +1264,7 @@ __global__ void __launch_bounds__(64 * (kBackWavesOf<G, FP, MODE, DUAL, W, QUAD>
     __shared__ __attribute__((aligned(16))) float2 decs[kFrontWaves][kDecBuf][kDec];
     __shared__ int mi_s[kGroups][2][QK_GROUP], rt_s[kGroups][2][QK_GROUP];
     // hunt tables: the MFMA correlator's B, or the FFT hunt's twiddles / Q / permutation
-    __shared__ __attribute__((aligned(16))) float BT[(MODE & 2) ? kFftHT : qhunt::kBT];
+    __shared__ __attribute__((aligned(16))) float BT[(MODE & 2) ? kFftHT : kHuntTab];
     __shared__ int bseq[kGroups][2], fcnt[kGroups][2];   // DUAL progress counters, per group
     const int lane = threadIdx.x & 63;
     // wave-uniform by construction; readfirstlane tells the compiler, so every
@@ -1256,7 +1276,11 @@ __global__ void __launch_bounds__(64 * (kBackWavesOf<G, FP, MODE, DUAL, W, QUAD>
     if constexpr ((MODE & 2) != 0) {
         for (int i = threadIdx.x; i < kFftHT; i += kBlock) BT[i] = fft_tab[i];
     } else {
+#if QPSK_HUNT_FILTER
+        qhunt::bconst_h_lds(threadIdx.x, kBlock, BT);
+#else
         qhunt::bconst_lds(threadIdx.x, kBlock, BT);
+#endif
     }
     if (wave < kGroups) {   // per-channel state of the groups at the call's first frame
         const int ch = (grp0 + wave) * W + lane;
