@@ -279,6 +279,17 @@ __device__ __forceinline__ void bconst_h_lds(int tid, int nthreads, float* BH) {
     }
 }
 
+// max over the 64 lanes of a wave (DPP row shifts / row broadcasts, no LDS trips)
+__device__ __forceinline__ unsigned wave_max_u32(unsigned v) {
+    v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false)); // row_shr:1
+    v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false)); // row_shr:2
+    v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xe, false)); // row_shr:4
+    v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xc, false)); // row_shr:8
+    v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false)); // row_bcast:15
+    v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false)); // row_bcast:31
+    return (unsigned)__builtin_amdgcn_readlane((int)v, 63);
+}
+
 // sum over the wave (DPP row shifts / broadcasts); order-free: only a bound
 template <int CTRL, int RM, int BM>
 __device__ __forceinline__ float dpp_f32(float x) {
@@ -394,6 +405,56 @@ __device__ __forceinline__ f4 correlate_pl(int lane, const float* TK, const floa
         acc = __builtin_amdgcn_mfma_f32_16x16x4f32(v.w, bl[16 * t + 12], acc, 0, 0, 0);
     }
     return acc;
+}
+
+// the writes of one wave's lanes visible to its other lanes' reads (LDS)
+__device__ __forceinline__ void lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// The reference's scan (src/qpsk.c:172-183) over exact sums: the first lag
+// whose cnormf (src/qpsk.c:75-80) is > the running max, which starts at 0.
+// Values are >= 0 or NaN (never selected): as non-negative float bits they
+// order as unsigned; take the wave max, then the lowest lag holding it; a
+// maximum of 0 leaves max_index at 0.  Lane order is lag order within each of
+// the two fragments (LO / HI map a lane to its lags).
+template <typename WaveMax, typename LO, typename HI>
+__device__ __forceinline__ int argmax_exact(f4 acc, WaveMax wave_max, LO lag_of_lo, HI lag_of_hi) {
+    const float r0 = acc[0], i0 = acc[1], r1 = acc[2], i1 = acc[3];
+    const float c0 = r0 * r0 + i0 * i0;
+    const float c1 = r1 * r1 + i1 * i1;
+    const unsigned k0 = c0 > 0.0f ? __float_as_uint(c0) : 0u;
+    const unsigned k1 = c1 > 0.0f ? __float_as_uint(c1) : 0u;
+    const unsigned km = wave_max(max(k0, k1));
+    if (km == 0u) return 0;
+    const unsigned long long m0 = __ballot(k0 == km), m1 = __ballot(k1 == km);
+    const int i0x = m0 ? lag_of_lo(__ffsll((long long)m0) - 1) : 1 << 20;
+    const int i1x = m1 ? lag_of_hi(__ffsll((long long)m1) - 1) : 1 << 20;
+    return min(i0x, i1x);
+}
+
+// max_index of dec's 128 lags on the matrix cores: the bf16 pass, and the
+// exact chain when it cannot decide (fb = true).  S: the wave's scratch (LDS,
+// >= max(kHBytes, 4 kTK) bytes, 16-B aligned); TB: bconst_h_lds's tables.
+template <typename WaveMax>
+__device__ __forceinline__ int hunt_index(int lane, const float2* dec, float* S, const float* TB,
+                                          WaveMax wave_max, bool& fb) {
+    char* H = reinterpret_cast<char*>(S);
+    const float W = store_h(lane, dec, H);
+    fb = false;
+    // an all-zero window (W sums non-negative terms: 0 only if every T is):
+    // every sum is 0, so no lag exceeds the initial max and max_index stays 0
+    if (W == 0.0f) return 0;
+    lds_sync();
+    const int pick = pick_h(lane, correlate_h(lane, H, TB), W, wave_max);
+    fb = pick < 0;
+    if (!fb) return pick;
+    lds_sync();   // the exact image overwrites H
+    store_t(lane, dec, S);
+    lds_sync();
+    return argmax_exact(correlate_pl(lane, S, TB + kBH), wave_max, lag_lo, lag_hi);
 }
 
 }  // namespace qhunt

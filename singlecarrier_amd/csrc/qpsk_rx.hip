@@ -274,16 +274,7 @@ __device__ __forceinline__ void mix(int lane, const int (&r)[kPf<MODE>], unsigne
     else mix_seq<MODE, false>(lane, r, P, M, kSeq);
 }
 
-// max over the 64 lanes of a wave (DPP row shifts / row broadcasts, no LDS trips)
-__device__ __forceinline__ unsigned wave_max_u32(unsigned v) {
-    v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false)); // row_shr:1
-    v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false)); // row_shr:2
-    v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xe, false)); // row_shr:4
-    v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xc, false)); // row_shr:8
-    v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false)); // row_bcast:15
-    v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false)); // row_bcast:31
-    return (unsigned)__builtin_amdgcn_readlane((int)v, 63);
-}
+using qhunt::wave_max_u32;
 
 // same, but volatile so the load/store optimizer does not pair it into a
 // ds_read2_b64 (8 LDS cycles per pair vs 2 per ds_read_b64: MI355X_MICROARCH.md)
@@ -439,37 +430,33 @@ __device__ __forceinline__ void fir_head(int lane, const float2* M, float2* dec)
 }
 
 // correlate (src/qpsk.c:88-96) for all 128 lags of dec and the hunt's argmax
-// (src/qpsk.c:172-183).  The T image reuses M (the FIR is done with it).
+// (src/qpsk.c:172-183).  The T images reuse M (the FIR is done with it).
 template <int MODE>
 __device__ __forceinline__ int hunt(int lane, float2* M, const float2* dec, const float* BT FACC_PARAM) {
 #ifdef QPSK_STAMPS
     unsigned long long ft0 = stamp_now();
 #endif
     if constexpr ((MODE & 2) != 0) return fft_hunt(lane, M, dec, BT);
-#if QPSK_HUNT_MFMA
-    // on the matrix cores (qpsk_hunt.h: bit-identical k-ordered chain)
-#if QPSK_HUNT_FILTER
-    {   // bf16 pass; certain argmax -> done
-        char* H = reinterpret_cast<char*>(M);
-        const float W = qhunt::store_h(lane, dec, H);
-        wave_lds_sync();
-        const int pick = qhunt::pick_h(lane, qhunt::correlate_h(lane, H, BT), W, wave_max_u32);
-        if (pick >= 0) return pick;
-        wave_lds_sync();   // the exact image below overwrites H
-    }
+#if QPSK_HUNT_MFMA && QPSK_HUNT_FILTER
+    // bf16 pass, exact chain when in doubt (qpsk_hunt.h hunt_index)
+    bool fb;
+    const int mi = qhunt::hunt_index(lane, dec, reinterpret_cast<float*>(M), BT, wave_max_u32, fb);
+#ifdef QPSK_STAMPS
+    facc[2] += 1;          // hunts
+    facc[3] += fb ? 1 : 0; // of which the exact chain decided
 #endif
+    FSTAMP(2);
+    return mi;
+#else
+#if QPSK_HUNT_MFMA
+    // exact chain only (qpsk_hunt.h: bit-identical k-ordered chain)
     float* TK = reinterpret_cast<float*>(M);
     qhunt::store_t(lane, dec, TK);
     wave_lds_sync();
     FSTAMP(2);
-#if QPSK_HUNT_FILTER
-    const qhunt::f4 acc = qhunt::correlate_pl(lane, TK, BT + qhunt::kBH);
-#else
     const qhunt::f4 acc = qhunt::correlate_bt(lane, TK, BT);
-#endif
     FSTAMP(3);
-#define QPSK_LAG_LO qhunt::lag_lo
-#define QPSK_LAG_HI qhunt::lag_hi
+    return qhunt::argmax_exact(acc, wave_max_u32, qhunt::lag_lo, qhunt::lag_hi);
 #else
     // as packed VALU chains (qpsk_hunt.h correlate_valu: the same k-ordered sums)
     float2* TV = M;
@@ -478,28 +465,9 @@ __device__ __forceinline__ int hunt(int lane, float2* M, const float2* dec, cons
     FSTAMP(2);
     const qhunt::f4 acc = qhunt::correlate_valu(lane, TV);
     FSTAMP(3);
-#define QPSK_LAG_LO qhunt::lag_lo_valu
-#define QPSK_LAG_HI qhunt::lag_hi_valu
+    return qhunt::argmax_exact(acc, wave_max_u32, qhunt::lag_lo_valu, qhunt::lag_hi_valu);
 #endif
-    const float r0 = acc[0], i0 = acc[1], r1 = acc[2], i1 = acc[3];
-    const float c0 = r0 * r0 + i0 * i0;    // cnormf, src/qpsk.c:75-80
-    const float c1 = r1 * r1 + i1 * i1;
-    // first lag whose value is > the running max, which starts at 0.  Values
-    // are >= 0 or NaN (never selected): map to non-negative float bits
-    // (monotone as unsigned), take the wave max, then the lowest lag holding
-    // it; a maximum of 0 leaves max_index at 0.  Lane order is lag order
-    // within each of the two fragments (qhunt::lag_lo/lag_hi).
-    const unsigned k0 = c0 > 0.0f ? __float_as_uint(c0) : 0u;
-    const unsigned k1 = c1 > 0.0f ? __float_as_uint(c1) : 0u;
-    const unsigned km = wave_max_u32(max(k0, k1));
-    FSTAMP(4);
-    if (km == 0u) return 0;
-    const unsigned long long m0 = __ballot(k0 == km), m1 = __ballot(k1 == km);
-    const int i0x = m0 ? QPSK_LAG_LO(__ffsll((long long)m0) - 1) : 1 << 20;
-    const int i1x = m1 ? QPSK_LAG_HI(__ffsll((long long)m1) - 1) : 1 << 20;
-#undef QPSK_LAG_LO
-#undef QPSK_LAG_HI
-    return min(i0x, i1x);
+#endif
 }
 
 // One channel of frame n's front: D_n (decimated with rx_timing rt), F_{n+1},

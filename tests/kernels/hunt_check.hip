@@ -36,3 +36,42 @@ extern "C" int hunt_check(const float2* dec, int n, float2* out) {
     (void)hipFree(d_out);
     return 0;
 }
+
+// The product's whole hunt decision (qhunt::hunt_index: bf16 pass, exact chain
+// when in doubt) on given decimated frames: out_idx[i] = max_index, out_fb[i] =
+// 1 when the exact chain decided.  tests/test_gpu_hunt.py compares max_index
+// with the reference's scan (src/qpsk.c:172-183) over its sequential sums.
+__global__ void __launch_bounds__(64) hunt_pick_kernel(const float2* dec, int* out_idx, int* out_fb) {
+    __shared__ __attribute__((aligned(16))) float TB[qhunt::kBH + qhunt::kPL];
+    __shared__ __attribute__((aligned(16))) float S[qhunt::kTK > qhunt::kHBytes / 4 ? qhunt::kTK : qhunt::kHBytes / 4];
+    __shared__ __attribute__((aligned(16))) float2 D[256];
+    const int lane = threadIdx.x;
+    qhunt::bconst_h_lds(lane, 64, TB);
+    const float2* d = dec + (size_t)blockIdx.x * 256;
+    for (int j = lane; j < 256; j += 64) D[j] = d[j];
+    __syncthreads();
+    bool fb;
+    const int mi = qhunt::hunt_index(lane, D, S, TB, qhunt::wave_max_u32, fb);
+    if (lane == 0) {
+        out_idx[blockIdx.x] = mi;
+        out_fb[blockIdx.x] = fb ? 1 : 0;
+    }
+}
+
+// dec: [n][256] float2 (entry 255 unused); out_idx, out_fb: [n]
+extern "C" int hunt_pick(const float2* dec, int n, int* out_idx, int* out_fb) {
+    float2* d_dec;
+    int *d_idx, *d_fb;
+    if (hipMalloc(&d_dec, sizeof(float2) * 256 * n) != hipSuccess) return -1;
+    if (hipMalloc(&d_idx, sizeof(int) * n) != hipSuccess) return -1;
+    if (hipMalloc(&d_fb, sizeof(int) * n) != hipSuccess) return -1;
+    (void)hipMemcpy(d_dec, dec, sizeof(float2) * 256 * n, hipMemcpyHostToDevice);
+    hunt_pick_kernel<<<n, 64>>>(d_dec, d_idx, d_fb);
+    if (hipDeviceSynchronize() != hipSuccess) return -2;
+    (void)hipMemcpy(out_idx, d_idx, sizeof(int) * n, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(out_fb, d_fb, sizeof(int) * n, hipMemcpyDeviceToHost);
+    (void)hipFree(d_dec);
+    (void)hipFree(d_idx);
+    (void)hipFree(d_fb);
+    return 0;
+}

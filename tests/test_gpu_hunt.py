@@ -23,6 +23,7 @@ def _lib():
         subprocess.run(["make", "-C", HERE], check=True)
     lib = C.CDLL(path)
     lib.hunt_check.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
+    lib.hunt_pick.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
     return lib
 
 
@@ -80,3 +81,87 @@ def test_mfma_correlator_bit_exact():
     assert not bad_re.any() and not bad_im.any(), (
         f"{int(bad_re.sum())} re / {int(bad_im.sum())} im sums differ, "
         f"first case {np.argwhere(bad_re | bad_im)[0]}")
+
+
+def ref_index(dec):
+    """The reference's hunt (src/qpsk.c:172-183): the first lag whose cnormf
+    (src/qpsk.c:75-80, fp32, no fusion) is > the running max from 0."""
+    re, im = ref_sums(dec)
+    c = (re * re + im * im).astype(np.float32)
+    best = np.zeros(c.shape[0], np.float32)
+    idx = np.zeros(c.shape[0], np.int64)
+    for lag in range(128):
+        up = c[:, lag] > best
+        best = np.where(up, c[:, lag], best)
+        idx = np.where(up, lag, idx)
+    return idx
+
+
+def _pick(dec):
+    n = dec.shape[0]
+    buf = np.zeros((n, 256, 2), np.float32)
+    buf[:, :255, 0] = dec.real
+    buf[:, :255, 1] = dec.imag
+    idx = np.zeros(n, np.int32)
+    fb = np.zeros(n, np.int32)
+    assert _lib().hunt_pick(buf.ctypes.data, n, idx.ctypes.data, fb.ctypes.data) == 0
+    return idx, fb
+
+
+def _frames(rng, n, amp, preamble):
+    """QPSK-like decimated windows: random symbols plus ISI-like jitter, with
+    the preamble (p_i (1 + j)) at a random lag when `preamble`."""
+    p = oracle.preamble().astype(np.float32)
+    sym = (rng.choice([-1, 1], (n, 255)) + 1j * rng.choice([-1, 1], (n, 255))) * 0.7
+    if preamble:
+        off = rng.integers(0, 128, n)
+        for k in range(n):
+            sym[k, off[k]:off[k] + 128] = p * (1 + 1j) * 0.7
+    sym = sym + 0.05 * (rng.standard_normal((n, 255)) + 1j * rng.standard_normal((n, 255)))
+    return (amp * sym).astype(np.complex64)
+
+
+def _near_ties(rng, n):
+    """Two preamble copies, at lags 0 and 127, whose amplitudes differ by a
+    relative eps from 0 to 1e-3: max_index flips between them around eps = 0,
+    and the bf16 pass must hand every case it cannot separate to the exact
+    chain."""
+    p = oracle.preamble().astype(np.float32)
+    eps = np.concatenate([[0.0], np.geomspace(1e-9, 1e-3, n // 2 - 1)])
+    eps = np.concatenate([eps, -eps])[:n]
+    dec = np.zeros((n, 255), np.complex64)
+    a = rng.uniform(0.3, 2.0, n)
+    for k in range(n):
+        dec[k, :128] += (p * (1 + 1j) * a[k]).astype(np.complex64)
+        dec[k, 127:255] += (p * (1 + 1j) * a[k] * (1 + eps[k])).astype(np.complex64)
+    dec += (1e-3 * (rng.standard_normal((n, 255)) + 1j * rng.standard_normal((n, 255)))).astype(np.complex64)
+    return dec.astype(np.complex64)
+
+
+def test_filtered_hunt_index_matches_reference():
+    """qhunt::hunt_index (the product's hunt: bf16 hi/lo pass with an error
+    bound, exact chain when in doubt) picks the reference's max_index on
+    typical frames at several amplitudes, exact ties (constant and all-zero
+    windows), constructed near-ties and the wide-exponent / cancellation /
+    subnormal / sparse cases; both paths are exercised."""
+    rng = np.random.default_rng(20261016)
+    parts = [_frames(rng, 512, a, pre) for a in (1.0, 1e-3, 4.0) for pre in (False, True)]
+    parts.append(_near_ties(rng, 512))
+    parts.append(_cases(rng, 256))
+    const = np.full((4, 255), 0.37 - 0.11j, np.complex64)
+    const[1] = 0.0
+    const[2] = 1e-30 + 0j
+    const[3, 200:] = 0.0                 # a truncated constant: no tie
+    parts.append(const)
+    dec = np.concatenate(parts)
+    idx, fb = _pick(dec)
+    ref = ref_index(dec)
+    bad = np.flatnonzero(idx != ref)
+    assert bad.size == 0, f"{bad.size} of {len(dec)} differ, first {bad[:5]}: {idx[bad[:5]]} vs {ref[bad[:5]]}"
+    # both paths ran: the bf16 pass decided most typical frames, the exact
+    # chain every tie (constant and zero windows) and the closest near-ties
+    n_typ = 6 * 512
+    assert fb[:n_typ].mean() < 0.05
+    assert fb[-4] == 1 and fb[-2] == 1   # constant (all lags tie), underflowing window
+    assert fb[-3] == 0                   # all-zero window: max_index 0 without the chain
+    assert fb[n_typ:n_typ + 512].sum() > 0 and fb[n_typ:n_typ + 512].mean() < 1.0
