@@ -1,4 +1,4 @@
 set -o pipefail
-timeout -k 10 300 python -u -m pytest tests/test_gpu_hunt.py -x -q --timeout 120 --timeout-method thread > gpurun_out/hunt_test.log 2>&1 &&
-timeout -k 10 300 python -u profiles/hunt_fallback.py > gpurun_out/hunt_fallback.txt 2>&1 &&
-timeout -k 10 300 python -u bench.py --cpu-channels 0 --cpu-all-channels 0 --stream-chunks 0 > gpurun_out/filt_bench2.json 2> gpurun_out/filt_bench2.err
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r02_pytest_gpu_v8.log 2>&1 &&
+timeout -k 10 400 python -u bench.py > gpurun_out/r02_bench_v8.json 2> gpurun_out/r02_bench_v8.err &&
+bash profiles/profile.sh r02_v8 > gpurun_out/r02_v8_profile.log 2>&1
