@@ -1,3 +1,2 @@
 set -o pipefail
-L=singlecarrier_amd/csrc/build
-bash profiles/ab.sh 3 $L/lib_hf1.so $L/lib_st0.so $L/lib_st6.so $L/lib_st20.so > gpurun_out/stagger2_ab.txt 2>&1
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -k "low_amplitude or edge_inputs" -x -q --timeout 120 --timeout-method thread > gpurun_out/lowamp.log 2>&1

@@ -119,6 +119,15 @@ def test_edge_inputs():
     _vs_oracle(x)
 
 
+@pytest.mark.parametrize("shift", [4, 8, 11])
+def test_low_amplitude_streams(shift):
+    """Synthetic streams scaled down by 2^shift (quantised to a few int16
+    levels at 11): correlations that tie exactly or nearly, which the
+    filtered hunt hands to the exact chain (qpsk_hunt.h hunt_index)."""
+    x = (oracle.synth(31 + shift, 256, 12, 8.0).astype(np.int32) >> shift).astype(np.int16)
+    _vs_oracle(x)
+
+
 def test_streaming_split_equals_one_call():
     """State (rx_timing, carried symbols, sample history, frame counter) persists
     across calls: feeding 16 frames as 5+1+1+9 == one 16-frame call."""
