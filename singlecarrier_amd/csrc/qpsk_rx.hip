@@ -1120,24 +1120,49 @@ struct JobX {
     }
 };
 
+#ifndef QPSK_DATA_RING
+#define QPSK_DATA_RING 4   // job samples loaded this many steps ahead (1: one step; profiles/r02_data_ring_ab.txt)
+#endif
+template <bool EXACT>
+__device__ __forceinline__ void data_step(Kal& k, f2 (&x)[5], f2 nx, int s, unsigned long long& dib,
+                                          float2* so, bool& bad) {
+    f2 sy = {0.0f, 0.0f};
+#pragma unroll
+    for (int t = 0; t < 5; t++) sy = sy + cmulc(x[t], k.eq[t]);
+    const int dI = sy.x < 0.0f, dQ = sy.y < 0.0f;
+    const f2 cst = {dI ? -1.0f : 1.0f, dQ ? -1.0f : 1.0f};
+    update_eq<EXACT>(k, x, (cst - sy) * 0.1f, bad);
+    dib |= (unsigned long long)(dQ | (dI << 1)) << (2 * s);
+    if (so) so[s] = make_float2(sy.x, sy.y);
+#pragma unroll
+    for (int t = 0; t < 4; t++) x[t] = x[t + 1];
+    x[4] = nx;
+}
+
 template <bool EXACT>
 __device__ __forceinline__ unsigned long long data_steps(Kal& k, f2 (&x)[5], const JobX xs,
                                                          float2* so, bool& bad) {
     unsigned long long dib = 0;
-    for (int s = 0; s < QK_NDSYM; s++) {
-        const f2 nx = xs[min(s + 5, 34)];
-        f2 sy = {0.0f, 0.0f};
+#if QPSK_DATA_RING > 1
+    // the job's samples arrive from HBM (written ~ms earlier by rx_kernel):
+    // each is loaded R steps before it enters x
+    constexpr int R = QPSK_DATA_RING;
+    f2 cur[R];
 #pragma unroll
-        for (int t = 0; t < 5; t++) sy = sy + cmulc(x[t], k.eq[t]);
-        const int dI = sy.x < 0.0f, dQ = sy.y < 0.0f;
-        const f2 cst = {dI ? -1.0f : 1.0f, dQ ? -1.0f : 1.0f};
-        update_eq<EXACT>(k, x, (cst - sy) * 0.1f, bad);
-        dib |= (unsigned long long)(dQ | (dI << 1)) << (2 * s);
-        if (so) so[s] = make_float2(sy.x, sy.y);
+    for (int t = 0; t < R; t++) cur[t] = xs[min(5 + t, 34)];
+    for (int s0 = 0; s0 < QK_NDSYM; s0 += R) {
+        f2 nxt[R];
 #pragma unroll
-        for (int t = 0; t < 4; t++) x[t] = x[t + 1];
-        x[4] = nx;
+        for (int t = 0; t < R; t++) nxt[t] = xs[min(s0 + R + 5 + t, 34)];
+#pragma unroll
+        for (int t = 0; t < R; t++)
+            if (s0 + t < QK_NDSYM) data_step<EXACT>(k, x, cur[t], s0 + t, dib, so, bad);
+#pragma unroll
+        for (int t = 0; t < R; t++) cur[t] = nxt[t];
     }
+#else
+    for (int s = 0; s < QK_NDSYM; s++) data_step<EXACT>(k, x, xs[min(s + 5, 34)], s, dib, so, bad);
+#endif
     return dib;
 }
 
