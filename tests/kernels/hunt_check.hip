@@ -75,3 +75,41 @@ extern "C" int hunt_pick(const float2* dec, int n, int* out_idx, int* out_fb) {
     (void)hipFree(d_fb);
     return 0;
 }
+
+// The bf16 pass alone (qhunt::store_h + correlate_h): every lag's (re, im)
+// approximate sum and the window's W, so tests/test_gpu_hunt.py can measure
+// |S' - S| / W on the hardware against the budget qpsk_hunt.h derives.
+__global__ void __launch_bounds__(64) hunt_h_kernel(const float2* dec, float2* out, float* out_w) {
+    __shared__ __attribute__((aligned(16))) float TB[qhunt::kBH + qhunt::kPL];
+    __shared__ __attribute__((aligned(16))) float S[qhunt::kHBytes / 4];
+    __shared__ __attribute__((aligned(16))) float2 D[256];
+    const int lane = threadIdx.x;
+    qhunt::bconst_h_lds(lane, 64, TB);
+    const float2* d = dec + (size_t)blockIdx.x * 256;
+    for (int j = lane; j < 256; j += 64) D[j] = d[j];
+    __syncthreads();
+    const float W = qhunt::store_h(lane, D, reinterpret_cast<char*>(S));
+    qhunt::lds_sync();
+    const qhunt::f4 acc = qhunt::correlate_h(lane, reinterpret_cast<const char*>(S), TB);
+    float2* o = out + (size_t)blockIdx.x * QK_NLAG;
+    o[qhunt::lag_lo(lane)] = make_float2(acc[0], acc[1]);
+    o[qhunt::lag_hi(lane)] = make_float2(acc[2], acc[3]);
+    if (lane == 0) out_w[blockIdx.x] = W;
+}
+
+extern "C" int hunt_h(const float2* dec, int n, float2* out, float* out_w) {
+    float2 *d_dec, *d_out;
+    float* d_w;
+    if (hipMalloc(&d_dec, sizeof(float2) * 256 * n) != hipSuccess) return -1;
+    if (hipMalloc(&d_out, sizeof(float2) * QK_NLAG * n) != hipSuccess) return -1;
+    if (hipMalloc(&d_w, sizeof(float) * n) != hipSuccess) return -1;
+    (void)hipMemcpy(d_dec, dec, sizeof(float2) * 256 * n, hipMemcpyHostToDevice);
+    hunt_h_kernel<<<n, 64>>>(d_dec, d_out, d_w);
+    if (hipDeviceSynchronize() != hipSuccess) return -2;
+    (void)hipMemcpy(out, d_out, sizeof(float2) * QK_NLAG * n, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(out_w, d_w, sizeof(float) * n, hipMemcpyDeviceToHost);
+    (void)hipFree(d_dec);
+    (void)hipFree(d_out);
+    (void)hipFree(d_w);
+    return 0;
+}

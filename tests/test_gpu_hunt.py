@@ -24,6 +24,7 @@ def _lib():
     lib = C.CDLL(path)
     lib.hunt_check.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
     lib.hunt_pick.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
+    lib.hunt_h.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
     return lib
 
 
@@ -165,3 +166,31 @@ def test_filtered_hunt_index_matches_reference():
     assert fb[-4] == 1 and fb[-2] == 1   # constant (all lags tie), underflowing window
     assert fb[-3] == 0                   # all-zero window: max_index 0 without the chain
     assert fb[n_typ:n_typ + 512].sum() > 0 and fb[n_typ:n_typ + 512].mean() < 1.0
+
+
+def test_bf16_pass_within_its_error_budget():
+    """The hardware side of the filtered hunt's proof: on the stress windows
+    the bf16 hi/lo pass (v_mfma_f32_16x16x32_bf16) lands within 2^-14.6 W of
+    the reference's sequential fp32 sums (plus 2^-110 for flushed denormals),
+    the budget qpsk_hunt.h derives and then covers 3x over (d = 2^-13 W +
+    2^-100); W as the kernel computes it bounds the exact sum of |Tr| + |Ti|."""
+    rng = np.random.default_rng(20261017)
+    dec = np.concatenate([_frames(rng, 512, 1.0, False), _frames(rng, 512, 3.0, True),
+                          _near_ties(rng, 256), _cases(rng, 256)])
+    n = dec.shape[0]
+    buf = np.zeros((n, 256, 2), np.float32)
+    buf[:, :255, 0] = dec.real
+    buf[:, :255, 1] = dec.imag
+    out = np.zeros((n, 128, 2), np.float32)
+    w = np.zeros(n, np.float32)
+    assert _lib().hunt_h(buf.ctypes.data, n, out.ctypes.data, w.ctypes.data) == 0
+    re, im = ref_sums(dec)
+    dr, di = dec.real.astype(np.float32), dec.imag.astype(np.float32)
+    w_exact = (np.abs(dr - di).astype(np.float64) + np.abs(di + dr)).sum(axis=1)
+    assert (w.astype(np.float64) >= w_exact * (1 - 2.0 ** -16)).all()
+    err = np.maximum(np.abs(out[..., 0].astype(np.float64) - re), np.abs(out[..., 1].astype(np.float64) - im))
+    # relative budget, plus the absolute allowance for denormal flushing
+    # (the subnormal windows: <= 2^-126 per term; the kernel's d adds 2^-100)
+    bound = 2.0 ** -14.6 * w_exact + 2.0 ** -110
+    excess = err.max(axis=1) / bound
+    assert excess.max() <= 1.0, (excess.max(), int(excess.argmax()))
