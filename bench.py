@@ -441,6 +441,13 @@ def main():
             roofline["traffic"] = p["hbm_bytes_per_launch"]
             roofline["traffic_source"] = p.get("source")
     valu = valu_from_counters(nch, nf, args.mode, t_launch)
+    # the minimal bit-exact formulation is ~96 fp32 ops per
+    # sample, 8.2e11 samples/s per GPU at 78.6e12 non-FMA packed ops/s
+    bound = {"samples_s_per_gpu": 8.2e11, "source": "SURVEY.md 8d (96 ops/sample minimal form)",
+             "frac": round(nch * nf * FRAME / t_launch / 8.2e11, 4)}
+    if valu is None:
+        valu = {}
+    valu["survey_minimal_form_bound"] = bound
 
     # parity spot check of the timed outputs on every rank (checker only; not
     # timed): the first k channels of the rank's shard
