@@ -1,3 +1,2 @@
 set -o pipefail
-L=singlecarrier_amd/csrc/build
-bash profiles/ab.sh 2 $L/lib_cur.so $L/lib_nostore.so > gpurun_out/nostore_ab.txt 2>&1
+timeout -k 10 1000 python -u bench.py --sweep > gpurun_out/r02_awgn_sweep_v5.jsonl 2> gpurun_out/r02_awgn_sweep_v5.err
