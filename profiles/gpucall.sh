@@ -1,2 +1,3 @@
 set -o pipefail
-timeout -k 10 1000 python -u bench.py --sweep > gpurun_out/r02_awgn_sweep_v5.jsonl 2> gpurun_out/r02_awgn_sweep_v5.err
+L=singlecarrier_amd/csrc/build
+bash profiles/ab.sh 3 $L/lib_bb0.so $L/lib_bb64.so $L/lib_bb96.so $L/lib_bb112.so > gpurun_out/boost_ab.txt 2>&1
