@@ -1,3 +1,2 @@
 set -o pipefail
-L=singlecarrier_amd/csrc/build
-bash profiles/ab.sh 3 $L/lib_bb0.so $L/lib_bb64.so $L/lib_bb96.so $L/lib_bb112.so > gpurun_out/boost_ab.txt 2>&1
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_dec752.py -k "low_amplitude" -x -q --timeout 120 --timeout-method thread > gpurun_out/lowamp2.log 2>&1

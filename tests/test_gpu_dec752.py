@@ -96,6 +96,14 @@ def test_every_workgroup_shape(shape, monkeypatch):
     _vs_oracle(x)
 
 
+@pytest.mark.parametrize("shift", [6, 11])
+def test_low_amplitude_streams(shift):
+    """The filtered hunt's near and exact ties (see test_gpu_parity.py) under
+    the dec752 semantics."""
+    x = (oracle.synth(41 + shift, 192, 12, 8.0).astype(np.int32) >> shift).astype(np.int16)
+    _vs_oracle(x)
+
+
 def test_streaming_split_equals_one_call():
     """The carried sample history is longer in this mode (x_{n-1}[0..1703]):
     feeding 16 frames as 1+4+2+9 == one call."""

@@ -119,11 +119,15 @@ def test_edge_inputs():
     _vs_oracle(x)
 
 
+@pytest.mark.parametrize("shape", [None, "4x2", "2x4d"])
 @pytest.mark.parametrize("shift", [4, 8, 11])
-def test_low_amplitude_streams(shift):
+def test_low_amplitude_streams(shift, shape, monkeypatch):
     """Synthetic streams scaled down by 2^shift (quantised to a few int16
     levels at 11): correlations that tie exactly or nearly, which the
-    filtered hunt hands to the exact chain (qpsk_hunt.h hunt_index)."""
+    filtered hunt hands to the exact chain (qpsk_hunt.h hunt_index); on the
+    default (dual-chain, quad) shape for this batch and forced 4x2 / 2x4d."""
+    if shape:
+        monkeypatch.setenv("QPSK_SHAPE", shape)
     x = (oracle.synth(31 + shift, 256, 12, 8.0).astype(np.int32) >> shift).astype(np.int16)
     _vs_oracle(x)
 
