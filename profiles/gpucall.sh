@@ -1,2 +1,3 @@
 set -o pipefail
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread > gpurun_out/r02_pytest_gpu_final.log 2>&1
+L=singlecarrier_amd/csrc/build
+bash profiles/ab.sh 3 $L/lib_cur.so $L/lib_dm3.so $L/lib_dm4.so $L/lib_dm0.so > gpurun_out/dmin_ab.txt 2>&1
