@@ -72,12 +72,18 @@ def init_host_group(rank: int, world: int):
     gloo's native code announces its peer connections on fd 1; the driver
     reads rank 0's stdout as the one JSON line, so fd 1 points at stderr
     while the group forms."""
+    import datetime
+
     import torch.distributed as dist
     sys.stdout.flush()
     saved = os.dup(1)
     os.dup2(2, 1)
     try:
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        # a bounded rendezvous/collective timeout: a rank that dies outside the
+        # launcher's watch (torch.distributed.run) cannot hold the others for
+        # gloo's default 30 minutes
+        dist.init_process_group("gloo", rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=300))
     finally:
         os.dup2(saved, 1)
         os.close(saved)
@@ -93,12 +99,14 @@ def free_port() -> int:
     return port
 
 
-def launch(nproc: int, argv, script: str = None, env=None) -> int:
+def launch(nproc: int, argv, script: str = None, env=None, poll_s: float = 0.2) -> int:
     """Run `script argv` as `nproc` ranks (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_*
     as torch.distributed.run sets them), one per GPU, and wait for all of
     them.  The launcher itself makes no GPU call (children are started before
-    anything here touches HIP, and by Popen, never exec).  Returns the worst
-    exit status."""
+    anything here touches HIP, and by Popen, never exec).  Every child is
+    watched: the first one to exit non-zero gets its peers terminated (they
+    would otherwise block in gloo's rendezvous or barrier until its timeout),
+    and its status is returned; 0 when every rank succeeds."""
     import subprocess
     script = script or os.path.abspath(__file__)
     port = free_port()
@@ -108,9 +116,23 @@ def launch(nproc: int, argv, script: str = None, env=None) -> int:
         e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nproc), LOCAL_WORLD_SIZE=str(nproc),
                  MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, script, *argv], env=e))
-    codes = [p.wait() for p in procs]
-    bad = [c for c in codes if c != 0]
-    return bad[0] if bad else 0
+    first_bad = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            rc = p.poll()
+            if rc is None:
+                continue
+            live.remove(p)
+            if rc != 0 and first_bad == 0:
+                first_bad = rc
+                for q in live:          # exact children of this launcher, by handle
+                    q.terminate()
+        if live:
+            time.sleep(poll_s)
+    for p in procs:
+        p.wait()
+    return first_bad
 
 
 def cpu_info() -> dict:
@@ -128,11 +150,19 @@ def cpu_info() -> dict:
         aff = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
         aff = None
-    return {"nproc": os.cpu_count(), "affinity_cpus": aff, "cpu_model": model,
-            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+    # the CPU time this job may use: cgroup v2 cpu.max ("quota period", or
+    # "max" for no limit), as CPUs
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        quota = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    return {"nproc": os.cpu_count(), "affinity_cpus": aff, "cgroup_cpu_quota": quota,
+            "cpu_model": model, "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -161,10 +191,14 @@ def parse():
     ap.add_argument("--sweep-frames", type=int, default=16)
     ap.add_argument("--sweep-points", type=str, default="0,1,2,3,4,5,6,7,8,9,10")
     ap.add_argument("--cpu-procs", type=int, default=16,
-                    help="host processes for the all-cores reference baseline and the sweep")
+                    help="host processes for the multi-core reference baseline and the sweep "
+                         "(16 = one GPU's share of the box's host cores)")
     ap.add_argument("--cpu-all-channels", type=int, default=32768,
-                    help="channels of the all-cores reference sample (0: skip)")
-    return ap.parse_args()
+                    help="channels of the multi-core reference sample (0: skip)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher/sharding rehearsal: every rank forms the host group, takes "
+                         "its shard and reduces a zero time, rank 0 prints the shards; no GPU use")
+    return ap.parse_args(argv)
 
 
 # ----------------------------------------------------------------- C5 sweep
@@ -299,21 +333,33 @@ def sweep(args):
                                                        for r in rows)}), flush=True)
 
 
-def valu_from_counters(nch: int, nf: int, mode: str, t_launch: float):
+def pmc_record(name: str, nch: int, nf: int, mode: str, khash: str, root: str = ROOT):
+    """A committed rocprofv3 counter record (profiles/pmc_traffic.json or
+    pmc_valu.json, written by profiles/summarize.py) when it describes THIS
+    workload and THIS build: same channels/frames/mode and the same
+    qpsk_kernel_hash() as the running library (the hash of the kernels'
+    sources and build rules).  Counters of another build are never reported."""
+    path = os.path.join(root, "profiles", name)
+    if not os.path.exists(path):
+        return None
+    p = json.load(open(path))
+    if p.get("channels") != nch or p.get("frames") != nf or p.get("mode", "reference") != mode:
+        return None
+    if not khash or p.get("kernel_hash") != khash:
+        return None
+    return p
+
+
+def valu_from_counters(p, t_launch: float):
     """VALU issue rate of rx_kernel + rx_data_kernel from MEASURED counters:
     SQ_INSTS_VALU (wave-instructions, every pass summed over the chip) per
-    launch, from the rocprofv3 --pmc pass of this build committed under
-    profiles/ (pmc_valu.json, written by profiles/summarize.py), over the
+    launch, from the rocprofv3 --pmc pass of this build (pmc_record), over the
     kernel time measured live here.  Peak: one wave64 VALU instruction per
     SIMD-32 per 2 cycles (MI355X_MICROARCH.md "Wave scheduling"), 1,024 SIMDs at
     2.4 GHz = 1.229e12 wave-instr/s; packed fp32 (v_pk_*) measured at 3.47
     cycles per wave-instruction per SIMD with two waves per SIMD
     (profiles/calib/valu_rate_r01.txt), i.e. 0.708e12 wave-instr/s."""
-    path = os.path.join(ROOT, "profiles", "pmc_valu.json")
-    if not os.path.exists(path):
-        return None
-    p = json.load(open(path))
-    if p.get("channels") != nch or p.get("frames") != nf or p.get("mode", "reference") != mode:
+    if p is None:
         return None
     insts = p["valu_insts_per_launch"]
     peak = VALU_SIMDS * VALU_CLOCK_GHZ * 1e9 / 2.0
@@ -322,12 +368,34 @@ def valu_from_counters(nch: int, nf: int, mode: str, t_launch: float):
     out = {"valu_insts_per_launch": insts, "achieved_winst_s": round(ach / 1e12, 4),
            "peak_winst_s": round(peak / 1e12, 4), "frac": round(ach / peak, 4),
            "packed_peak_winst_s": round(peak_pk / 1e12, 4), "frac_packed": round(ach / peak_pk, 4),
-           "unit": "1e12 wave64 VALU instructions/s", "source": p.get("source")}
+           "unit": "1e12 wave64 VALU instructions/s", "source": p.get("source"),
+           "kernel_hash": p.get("kernel_hash")}
     if p.get("active_valu_frac") is not None:
         out["sq_active_inst_valu_per_wave_cycle"] = p["active_valu_frac"]
     if p.get("clock_ghz") is not None:
         out["clock_ghz_under_profiler"] = p["clock_ghz"]
     return out
+
+
+def dry_run(args, world: int, rank: int, local: int, strong: bool) -> None:
+    """The multi-rank path up to the first GPU call: host group, shard,
+    timing reduction, gather of the per-rank records; rank 0 prints one JSON
+    line.  Lets a CPU test run `bench.py --gpus N --dry-run` end to end."""
+    dist = init_host_group(rank, world) if world > 1 else None
+    nch, c0 = shard(args.channels, world, rank, strong)
+    tmax, total = reduce_step(dist, 0.001 * (rank + 1), nch)
+    rec = {"rank": rank, "local_rank": local, "channels": [c0, c0 + nch]}
+    recs = [rec]
+    if dist:
+        recs = [None] * world
+        dist.all_gather_object(recs, rec)
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "world": world, "channels_total": total,
+                          "max_time_s": tmax, "shards": recs,
+                          "scaling": "strong" if strong else "weak"}), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 def main():
@@ -341,6 +409,8 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     strong = not args.weak
+    if args.dry_run:
+        return dry_run(args, world, rank, local, strong)
     pool = None
     if rank == 0 and args.cpu_all_channels > 0 and args.cpu_procs > 1:
         import multiprocessing as mp
@@ -434,13 +504,13 @@ def main():
                 "kernels_us": {"rx_kernel": round(rx_ms / args.steps * 1e3, 2),
                                "rx_data_kernel": round(data_ms / args.steps * 1e3, 2)},
                 "alg_bytes_per_launch": alg_bytes}
-    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc):
-        p = json.load(open(pmc))
-        if p.get("channels") == nch and p.get("frames") == nf and p.get("mode", "reference") == args.mode:
-            roofline["traffic"] = p["hbm_bytes_per_launch"]
-            roofline["traffic_source"] = p.get("source")
-    valu = valu_from_counters(nch, nf, args.mode, t_launch)
+    khash = sc.kernel_hash()
+    roofline["kernel_hash"] = khash
+    p = pmc_record("pmc_traffic.json", nch, nf, args.mode, khash)
+    if p is not None:
+        roofline["traffic"] = p["hbm_bytes_per_launch"]
+        roofline["traffic_source"] = p.get("source")
+    valu = valu_from_counters(pmc_record("pmc_valu.json", nch, nf, args.mode, khash), t_launch)
     # the minimal bit-exact formulation is ~96 fp32 ops per
     # sample, 8.2e11 samples/s per GPU at 78.6e12 non-FMA packed ops/s
     bound = {"samples_s_per_gpu": 8.2e11, "source": "SURVEY.md 8d (96 ops/sample minimal form)",

@@ -100,9 +100,13 @@ int qpsk_rx_batch_device(qpsk_ctx *ctx, const int16_t *d_in, int nframes,
                          uint8_t *d_bits, uint8_t *d_valid, int32_t *d_trace,
                          float *d_soft, void *stream);
 
-/* Waits for the context's latest qpsk_rx_batch_device call (its stream) and
- * returns QPSK_ESTALL if any call since the previous check reported a
- * device-side failure (the device error word is sticky until read), else 0. */
+/* Waits for the context's latest qpsk_rx_batch_device call (an event recorded
+ * on its stream after its kernels; the stream itself may since be destroyed)
+ * and returns QPSK_ESTALL if any call since the previous check reported a
+ * device-side failure, else 0.  The device error word is sticky until this
+ * reads it, and is read and cleared in one atomic exchange.  Calls on one
+ * context depend on each other through the per-channel state, so the caller
+ * orders them (one stream, or streams it chains). */
 int qpsk_rx_sync(qpsk_ctx *ctx);
 
 /* Kernel-time accounting.  When enabled, every qpsk_rx_batch_device call
@@ -116,6 +120,12 @@ int qpsk_rx_timing_split(qpsk_ctx *ctx, float *ms_rx, float *ms_data, int *frame
 
 /* Message for an error code (static storage). */
 const char *qpsk_strerror(int err);
+
+/* Provenance of the receive kernels in this library: the first 16 hex digits of
+ * the sha256 of their sources and build rules (singlecarrier_amd/csrc/Makefile
+ * KSRC).  Profiled counters record it; bench.py reports them only for a
+ * library with the same hash. */
+const char *qpsk_kernel_hash(void);
 
 #ifdef __cplusplus
 }

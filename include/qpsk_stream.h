@@ -47,7 +47,9 @@ int qpsk_stream_submit(qpsk_stream *s);
 /* chunks submitted and not yet retrieved */
 int qpsk_stream_pending(const qpsk_stream *s);
 /* wait for the oldest submitted chunk; *bits / *valid point into its pinned
- * output buffers (layouts as qpsk_rx_batch) */
+ * output buffers (layouts as qpsk_rx_batch).  Returns QPSK_ESTALL (qpsk_batch.h)
+ * when a device-side progress wait of that chunk's receive ran out: its
+ * outputs are then undefined (the chunk counts as retrieved either way). */
 int qpsk_stream_retrieve(qpsk_stream *s, const uint8_t **bits, const uint8_t **valid);
 /* the stream's receiver (e.g. for qpsk_rx_frames / qpsk_rx_reset between streams) */
 struct qpsk_ctx *qpsk_stream_ctx(qpsk_stream *s);

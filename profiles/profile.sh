@@ -8,6 +8,8 @@ TAG=${1:-run}; shift || true
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
+# provenance of the profiled kernels (summarize.py -> pmc_*.json -> bench.py)
+python3 -c "import singlecarrier_amd as sc; print(sc.kernel_hash())" > $OUT/kernel_hash.txt
 B="bench.py --steps 5 --warmup 2 --cpu-channels 0 --cpu-all-channels 0 --stream-chunks 0 --verify 0 $*"
 run() { # name, rocprof args...
   local name=$1; shift

@@ -1,0 +1,26 @@
+#!/bin/bash
+# One GPU call of round 3: the -m gpu suite, the default bench line and the
+# rocprofv3 passes of profile.sh, every step under its own time limit; a crash,
+# abort or time-out (exit status >= 124) ends the call there.  Outputs go to
+# gpurun_out/c<N>_* (suffixed by call number, never overwritten).
+#   bash profiles/r03_call.sh N [tests|bench|prof|env]...
+set -u
+N=$1; shift
+O=gpurun_out/c${N}
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+check() { # name rc
+  echo "[$(date +%T)] $1 rc=$2" >&2
+  if [ "$2" -ge 124 ]; then echo "stopping: $1 rc=$2" >&2; exit "$2"; fi
+}
+for what in "$@"; do
+  echo "[$(date +%T)] $what" >&2
+  case $what in
+    tests) timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 300 \
+             --timeout-method thread > ${O}_pytest.log 2>&1; check pytest $? ;;
+    bench) timeout -k 10 400 python bench.py > ${O}_bench.json 2> ${O}_bench.err; check bench $? ;;
+    prof)  timeout -k 10 900 bash profiles/profile.sh r03_c${N}; check prof $? ;;
+    env)   { nproc; cat /sys/fs/cgroup/cpu.max; python3 -c "import os; print(len(os.sched_getaffinity(0)))"; } > ${O}_env.txt 2>&1 ;;
+    *) echo "unknown step $what" >&2; exit 2 ;;
+  esac
+done

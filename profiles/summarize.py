@@ -4,7 +4,9 @@ launch with the gfx950 FETCH_SIZE correction (MI355X_MICROARCH.md 'HBM':
 FETCH_SIZE counts half the bytes of wide coalesced reads -> x2), the VALU
 instruction count per launch (SQ_INSTS_VALU) and the LDS bank-conflict share;
 writes profiles/<tag>_summary.md, profiles/pmc_traffic.json and
-profiles/pmc_valu.json (bench.py reads the last two when the workload matches).
+profiles/pmc_valu.json (bench.py reads the last two when the workload AND the
+kernel hash match: the run directory's kernel_hash.txt, written by profile.sh
+from the profiled library's qpsk_kernel_hash()).
 
     python profiles/summarize.py gpurun_out/prof_v1 TAG CHANNELS FRAMES [SKIP [COUNT]]
 
@@ -106,10 +108,17 @@ if valu_insts:
     lines.append(f"- VALU wave-instructions per step (SQ_INSTS_VALU, both kernels): {valu_insts:.4g}; "
                  f"issue rate {valu_insts / t_step:.4g} per ns vs peak 1,024 SIMDs / 2 cycles x 2.4 GHz "
                  f"= 1228.8 per ns: {valu_insts / t_step / 1228.8:.3f}")
+# the profiled library's qpsk_kernel_hash() (profile.sh writes it next to the
+# runs): bench.py reports these counters only for a library with that hash
+khash = None
+kh_path = os.path.join(d, "kernel_hash.txt")
+if os.path.exists(kh_path):
+    khash = open(kh_path).read().strip() or None
+lines.append(f"- kernel hash (qpsk_kernel_hash of the profiled library): {khash}")
 open(os.path.join("profiles", f"{tag}_summary.md"), "w").write("\n".join(lines) + "\n")
 json.dump({"channels": nch, "frames": nfr, "hbm_bytes_per_launch": int(fetch_b + write_b),
            "kernels": [K, KD],
-           "fetch_bytes": int(fetch_b), "write_bytes": int(write_b),
+           "fetch_bytes": int(fetch_b), "write_bytes": int(write_b), "kernel_hash": khash,
            "source": f"profiles/{tag}_summary.md (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes)"},
           open(os.path.join("profiles", "pmc_traffic.json"), "w"), indent=1)
 if valu_insts:
@@ -117,7 +126,7 @@ if valu_insts:
                "valu_insts_per_launch": int(valu_insts),
                "active_valu_frac": (round(c["SQ_ACTIVE_INST_VALU"] / c["SQ_WAVE_CYCLES"], 4)
                                     if "SQ_ACTIVE_INST_VALU" in c and "SQ_WAVE_CYCLES" in c else None),
-               "clock_ghz": round(clock, 3) if clock else None,
+               "clock_ghz": round(clock, 3) if clock else None, "kernel_hash": khash,
                "source": f"profiles/{tag}_summary.md (rocprofv3 --pmc SQ_INSTS_VALU pass)"},
               open(os.path.join("profiles", "pmc_valu.json"), "w"), indent=1)
 print("\n".join(lines))

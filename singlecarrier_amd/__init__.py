@@ -54,6 +54,29 @@ def build(verbose: bool = False) -> str:
     return LIB_PATH
 
 
+# the receive kernels' sources and build rules, in the order the Makefile's KSRC
+# hashes them (csrc/Makefile: qpsk_kernel_hash())
+KERNEL_SOURCES = ("qpsk_rx.hip", "qpsk_hunt.h", "qpsk_rcp.h", "qpsk_consts.h", "qpsk_fft_dev.h",
+                  "qpsk_fft_tables.h", "qpsk_rx_internal.h", "Makefile")
+
+
+def kernel_source_hash(csrc: str = None) -> str:
+    """The hash the Makefile compiles into the library, from the sources in
+    `csrc` (default: this package's csrc/)."""
+    import hashlib
+    csrc = csrc or os.path.join(HERE, "csrc")
+    h = hashlib.sha256()
+    for name in KERNEL_SOURCES:
+        with open(os.path.join(csrc, name), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def kernel_hash() -> str:
+    """qpsk_kernel_hash() of the loaded library (no GPU needed)."""
+    return lib().qpsk_kernel_hash().decode()
+
+
 def lib():
     """Load the HIP library (fails loudly when it is missing)."""
     global _lib
@@ -81,6 +104,8 @@ def lib():
         L.qpsk_rx_batch_device.argtypes = [vp, vp, i32, vp, vp, vp, vp, vp]
         L.qpsk_strerror.restype = C.c_char_p
         L.qpsk_strerror.argtypes = [i32]
+        L.qpsk_kernel_hash.restype = C.c_char_p
+        L.qpsk_kernel_hash.argtypes = []
         L.qpsk_rx_frame.argtypes = [vp, vp]
         L.qpsk_tx_frame.argtypes = [vp, vp, i32, C.c_bool]
         L.qpsk_surface_error.restype = i32
@@ -124,6 +149,7 @@ def lib():
 
 SYMBOLS = ["qpsk_rx_create", "qpsk_rx_create_mode", "qpsk_rx_mode", "qpsk_rx_destroy", "qpsk_rx_reset", "qpsk_rx_channels",
            "qpsk_rx_frames", "qpsk_rx_batch", "qpsk_rx_batch_device", "qpsk_rx_sync", "qpsk_strerror",
+           "qpsk_kernel_hash",
            "cnormf", "qpsk_mod", "qpsk_demod", "qpsk_rx_frame", "qpsk_tx_frame",
            "qpsk_rx_init", "qpsk_tx_init", "qpsk_surface_error", "qpsk_tx_state_init",
            "qpsk_tx_frame_state", "qpsk_synth_batch", "qpsk_rx_timing_enable",

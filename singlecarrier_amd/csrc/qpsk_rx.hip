@@ -35,6 +35,7 @@
 #include "qpsk_fft_tables.h"
 #include "qpsk_hunt.h"
 #include "qpsk_rcp.h"
+#include "qpsk_rx_internal.h"
 
 #pragma clang fp contract(off)
 
@@ -144,20 +145,29 @@ __device__ __forceinline__ void wave_lds_sync() {
 // is resident, and every counter is advanced by every frame of its producer,
 // so each wait ends.  The bound keeps a logic error from hanging the GPU: a
 // wait that runs out sets kErrStall in the call's device error word, which
-// the host returns as QPSK_ESTALL (qpsk_rx_sync / qpsk_rx_batch), so stale
-// windows or rx_timing never pass as a result.
+// the host returns as QPSK_ESTALL (qpsk_rx_sync / qpsk_rx_batch /
+// qpsk_stream_retrieve), so stale windows or rx_timing never pass as a result.
+// The timeout is sticky per workgroup: it also sets the LDS word `dead`, and
+// every later wait of the workgroup returns at once, so a broken counter costs
+// one bound per workgroup, not one per frame.
 constexpr unsigned kSpinBound = 1u << 22;   // ~0.1 s; a frame is ~2.5k spins
 constexpr int kErrStall = 1;                // device error word bits
 
-__device__ __forceinline__ void spin_wait(int* p, int v, int* err, unsigned bound = kSpinBound) {
+__device__ __forceinline__ void spin_wait(int* p, int v, int* err, int* dead,
+                                          unsigned bound = kSpinBound) {
     unsigned it = 0;
     for (; it < bound; it++) {
         const int c = __builtin_amdgcn_readfirstlane(
             __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-        if (c >= v) break;
+        const int d = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_load(dead, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+        if (c >= v || d != 0) break;
         __builtin_amdgcn_s_sleep(1);
     }
-    if (it == bound && __lane_id() == 0) atomicOr(err, kErrStall);
+    if (it == bound && __lane_id() == 0) {
+        __hip_atomic_store(dead, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        atomicOr(err, kErrStall);
+    }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
@@ -1259,6 +1269,7 @@ __global__ void __launch_bounds__(64 * (kBackWavesOf<G, FP, MODE, DUAL, W, QUAD>
     // hunt tables: the MFMA correlator's B, or the FFT hunt's twiddles / Q / permutation
     __shared__ __attribute__((aligned(16))) float BT[(MODE & 2) ? kFftHT : kHuntTab];
     __shared__ int bseq[kGroups][2], fcnt[kGroups][2];   // DUAL progress counters, per group
+    __shared__ int dead_s;                               // DUAL: a wait of this workgroup timed out
     const int lane = threadIdx.x & 63;
     // wave-uniform by construction; readfirstlane tells the compiler, so every
     // per-wave index and pointer below lives in SGPRs
@@ -1283,6 +1294,7 @@ __global__ void __launch_bounds__(64 * (kBackWavesOf<G, FP, MODE, DUAL, W, QUAD>
         }
     }
     if (threadIdx.x < 2 * kGroups) (&bseq[0][0])[threadIdx.x] = (&fcnt[0][0])[threadIdx.x] = 0;
+    if (threadIdx.x == 0) dead_s = 0;
     __syncthreads();
     if constexpr (DUAL) {
         // bseq[gi][p]: frames of parity p decided, summed over the chain's back
@@ -1300,19 +1312,19 @@ __global__ void __launch_bounds__(64 * (kBackWavesOf<G, FP, MODE, DUAL, W, QUAD>
             // tests (roles bit kDebugStall): one wait that cannot end, on the
             // first back wave of workgroup 0, with a short bound
             if ((a.roles & kDebugStall) && blockIdx.x == 0 && wave == 0)
-                spin_wait(&fcnt[gi][0], 1 << 30, a.err, 1u << 12);
+                spin_wait(&fcnt[gi][0], 1 << 30, a.err, &dead_s, 1u << 12);
             // diagnostic stamps (QPSK_STAMPS): 13 frame work, 14 wait for the
             // fronts, 15 wait for the other chain's decision
             STAMP_DECL
             for (int n = wave & 1; n < a.F; n += 2) {
                 const int p = n & 1;
                 // front(n-1) done by every front wave of the group: window n and mi_n
-                if (n > 0) spin_wait(&fcnt[gi][p ^ 1], kFrontPer * ((n - 1) / 2 + 1), a.err);
+                if (n > 0) spin_wait(&fcnt[gi][p ^ 1], kFrontPer * ((n - 1) / 2 + 1), a.err, &dead_s);
                 STAMP(14);
                 const int mi = mi_s[gi][p][idx];
                 auto get_rt = [&] {   // rx_timing of frame n = the decision of frame n-1
                     STAMP(13);
-                    if (n > 0) spin_wait(&bseq[gi][p ^ 1], decided(n - 1), a.err);
+                    if (n > 0) spin_wait(&bseq[gi][p ^ 1], decided(n - 1), a.err, &dead_s);
                     STAMP(15);
                     return rt_s[gi][p][idx];
                 };
@@ -1355,7 +1367,7 @@ __global__ void __launch_bounds__(64 * (kBackWavesOf<G, FP, MODE, DUAL, W, QUAD>
                 float2* wout = win_of(a, g + 1u);
                 // back(n-1) done: rx_timing of frame n, and window n+1's buffer
                 // (window n-1) and mi_s[p ^ 1] (mi_{n-1}) are free
-                if (n > 0) spin_wait(&bseq[gi][p ^ 1], decided(n - 1), a.err);
+                if (n > 0) spin_wait(&bseq[gi][p ^ 1], decided(n - 1), a.err, &dead_s);
                 STAMP(7);
                 int pmi = 0;
                 for (int c = 0; c < nlive; c++) {
@@ -1539,8 +1551,10 @@ struct qpsk_ctx {
     int width = 0;              // dual-chain group width forced by QPSK_WIDTH; 0: by batch size
     int quad = -1;              // quad-per-channel backs forced on/off by QPSK_QUAD; -1: by width
     int prio = -1;              // issue priority forced by QPSK_PRIO (0 none, 1 front, 2 back)
-    int* d_err = nullptr;       // device error word (kErrStall), cleared by qpsk_rx_sync
-    hipStream_t last = nullptr; // stream of the latest qpsk_rx_batch_device call
+    int* d_err = nullptr;       // [0] device error word (kErrStall), taken by qpsk_rx_sync;
+                                // [1] the value it took
+    hipEvent_t done = nullptr;  // recorded after the latest call's kernels, on its stream
+    bool called = false;        // `done` has been recorded
     float pend_ms[2] = {0.0f, 0.0f};
     int pend_frames = 0;
 };
@@ -1587,7 +1601,8 @@ static int ctx_alloc(qpsk_ctx* c) {
     HCHECK(hipMalloc(&c->d_ks, sizeof(unsigned long long) * QK_KS_FRAMES));
     HCHECK(hipMalloc(&c->d_hist, sizeof(int16_t) * nslot(c) * 2 * QK_FRAME));
     HCHECK(hipMalloc(&c->d_njobs, sizeof(unsigned) * 2));
-    HCHECK(hipMalloc(&c->d_err, sizeof(int)));
+    HCHECK(hipMalloc(&c->d_err, 2 * sizeof(int)));
+    HCHECK(hipEventCreateWithFlags(&c->done, hipEventDisableTiming));
     for (int p = 0; p < 2; p++) {
         HCHECK(hipMalloc(&c->d_win[p], sizeof(float2) * nslot(c) * kWinStride));
         HCHECK(hipMalloc(&c->d_mi[p], sizeof(int) * nslot(c)));
@@ -1602,7 +1617,7 @@ extern "C" int qpsk_rx_reset(qpsk_ctx* c) {
     const size_t ns = nslot(c);
     HCHECK(hipMemsetAsync(c->d_hist, 0, sizeof(int16_t) * ns * 2 * QK_FRAME, c->stream));
     HCHECK(hipMemsetAsync(c->d_njobs, 0, sizeof(unsigned) * 2, c->stream));
-    HCHECK(hipMemsetAsync(c->d_err, 0, sizeof(int), c->stream));
+    HCHECK(hipMemsetAsync(c->d_err, 0, 2 * sizeof(int), c->stream));
     for (int p = 0; p < 2; p++) {
         HCHECK(hipMemsetAsync(c->d_win[p], 0, sizeof(float2) * ns * kWinStride, c->stream));
         HCHECK(hipMemsetAsync(c->d_mi[p], 0, sizeof(int) * ns, c->stream));
@@ -1626,6 +1641,7 @@ static void ctx_free(qpsk_ctx* c) {
             if (c->ev[i][j]) (void)hipEventDestroy(c->ev[i][j]);
     (void)hipFree(c->d_ptab);
     (void)hipFree(c->d_err);
+    if (c->done) (void)hipEventDestroy(c->done);
     (void)hipFree(c->d_jobs);
     (void)hipFree(c->d_njobs);
     (void)hipFree(c->d_ks);
@@ -1787,14 +1803,17 @@ static Shape pick_shape(const qpsk_ctx* c) {
     return sh;
 }
 
-extern "C" int qpsk_rx_batch_device(qpsk_ctx* c, const int16_t* d_in, int F, uint8_t* d_bits,
-                                    uint8_t* d_valid, int32_t* d_trace, float* d_soft,
-                                    void* stream) {
+// The two launches of a call (qpsk_rx_batch_device), with the device error word
+// the call's progress waits report to: the context's (qpsk_rx_sync takes it),
+// or a caller's own (qpsk_stream.hip: one per stream slot, so a stall is
+// reported with the chunk it belongs to).
+int qpsk_rx_launch(qpsk_ctx* c, const int16_t* d_in, int F, uint8_t* d_bits, uint8_t* d_valid,
+                   int32_t* d_trace, float* d_soft, hipStream_t s, int* d_err) {
     if (!c || F < 0 || (F > 0 && (!d_in || !d_bits || !d_valid))) return QPSK_EINVAL;
     if (F == 0) return QPSK_OK;
     if ((reinterpret_cast<uintptr_t>(d_in) & 15u) != 0) return QPSK_EINVAL;  // int4 loads
     HCHECK(hipSetDevice(c->device));
-    hipStream_t s = (hipStream_t)stream;
+    if (!d_err) d_err = c->d_err;
     const size_t need = (size_t)c->nch * (size_t)F;   // every frame valid, at most
     // job slots are addressed with 32-bit byte offsets (slot * 16); 2^28 channel-
     // frames would be 1 TB of input, beyond any device's memory
@@ -1835,7 +1854,7 @@ extern "C" int qpsk_rx_batch_device(qpsk_ctx* c, const int16_t* d_in, int F, uin
                        c->d_rt[1], d_bits, d_valid, d_trace, reinterpret_cast<float2*>(d_soft), \
                        c->d_jobs, c->d_njobs + parity, c->nch, F,                               \
                        (unsigned)(c->frames & 0xffffffffu), sh.roles, c->d_fft,                \
-                       (unsigned long long)c->jobs_cap, c->d_err)
+                       (unsigned long long)c->jobs_cap, d_err)
 #define QPSK_LAUNCH_MODE(MM)                                                                   \
     do {                                                                                       \
         switch (sh.kind) {                                                                     \
@@ -1863,24 +1882,43 @@ extern "C" int qpsk_rx_batch_device(qpsk_ctx* c, const int16_t* d_in, int F, uin
                        reinterpret_cast<float2*>(d_soft), parity, c->roles & kForceExact);
     HCHECK(hipGetLastError());
     if (slot >= 0) HCHECK(hipEventRecord(c->ev[slot][2], s));
+    HCHECK(hipEventRecord(c->done, s));
+    c->called = true;
     c->frames += (uint64_t)F;
     c->calls++;
-    c->last = s;
     return QPSK_OK;
 }
 
-// Waits for the context's latest call and reports a device-side failure of any
-// call since the previous check (the error word is sticky until read).
+extern "C" int qpsk_rx_batch_device(qpsk_ctx* c, const int16_t* d_in, int F, uint8_t* d_bits,
+                                    uint8_t* d_valid, int32_t* d_trace, float* d_soft,
+                                    void* stream) {
+    return qpsk_rx_launch(c, d_in, F, d_bits, d_valid, d_trace, d_soft, (hipStream_t)stream,
+                          nullptr);
+}
+
+namespace {
+// read and clear the error word in one atomic exchange: a stall reported by a
+// kernel between a read and a separate clear cannot be lost
+__global__ void err_take_kernel(int* err) {
+    if (threadIdx.x == 0) err[1] = atomicExch(&err[0], 0);
+}
+}  // namespace
+
+// Waits for the context's latest call (an event recorded on its stream, so the
+// stream may since have been destroyed) and reports a device-side failure of
+// any call since the previous check.  Calls on one context depend on each
+// other through the per-channel state, so they are ordered (one stream, or
+// streams the caller chains); the latest call's completion covers them all.
 extern "C" int qpsk_rx_sync(qpsk_ctx* c) {
     if (!c) return QPSK_EINVAL;
     HCHECK(hipSetDevice(c->device));
-    HCHECK(hipStreamSynchronize(c->last));
-    HCHECK(hipStreamSynchronize(c->stream));
+    if (c->called) HCHECK(hipEventSynchronize(c->done));
+    hipLaunchKernelGGL(err_take_kernel, dim3(1), dim3(64), 0, c->stream, c->d_err);
+    HCHECK(hipGetLastError());
     int e = 0;
-    HCHECK(hipMemcpy(&e, c->d_err, sizeof e, hipMemcpyDeviceToHost));
-    if (e == 0) return QPSK_OK;
-    HCHECK(hipMemset(c->d_err, 0, sizeof(int)));
-    return QPSK_ESTALL;
+    HCHECK(hipMemcpyAsync(&e, c->d_err + 1, sizeof e, hipMemcpyDeviceToHost, c->stream));
+    HCHECK(hipStreamSynchronize(c->stream));
+    return e == 0 ? QPSK_OK : QPSK_ESTALL;
 }
 
 extern "C" int qpsk_rx_timing_enable(qpsk_ctx* c, int on) {
@@ -1974,6 +2012,12 @@ extern "C" int qpsk_debug_stamps(unsigned long long* out16, int reset) {
     return 0;
 }
 #endif
+
+#ifndef QPSK_KERNEL_HASH
+#define QPSK_KERNEL_HASH "unknown"
+#endif
+// the Makefile's hash of the receive kernels' sources and build rules
+extern "C" const char* qpsk_kernel_hash(void) { return QPSK_KERNEL_HASH; }
 
 extern "C" const char* qpsk_strerror(int err) {
     switch (err) {

@@ -1,0 +1,14 @@
+// qpsk_rx_internal.h -- entry points shared inside libqpsk_hip.so (not part of
+// the C-ABI in include/).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "qpsk_batch.h"
+
+// qpsk_rx_batch_device() with the device error word the call's progress waits
+// report stalls to (nullptr: the context's own, which qpsk_rx_sync() takes).
+// qpsk_stream.hip gives each stream slot its own word, so a stall is reported
+// by qpsk_stream_retrieve() for the chunk it happened in.
+int qpsk_rx_launch(qpsk_ctx* c, const int16_t* d_in, int F, uint8_t* d_bits, uint8_t* d_valid,
+                   int32_t* d_trace, float* d_soft, hipStream_t s, int* d_err);

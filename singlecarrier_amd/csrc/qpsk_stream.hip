@@ -9,6 +9,7 @@
 
 #include "qpsk_batch.h"
 #include "qpsk_consts.h"
+#include "qpsk_rx_internal.h"
 #include "qpsk_stream.h"
 
 namespace {
@@ -22,6 +23,8 @@ struct Slot {
     uint8_t* d_valid = nullptr;
     uint8_t* h_bits = nullptr;   // pinned
     uint8_t* h_valid = nullptr;  // pinned
+    int* d_err = nullptr;        // the chunk's device error word (progress-wait stalls)
+    int* h_err = nullptr;        // pinned copy, read by qpsk_stream_retrieve
     hipEvent_t copied = nullptr, received = nullptr, done = nullptr;
 };
 
@@ -46,6 +49,8 @@ static void stream_free(qpsk_stream* s) {
         (void)hipHostFree(q.h_in);
         (void)hipHostFree(q.h_bits);
         (void)hipHostFree(q.h_valid);
+        (void)hipHostFree(q.h_err);
+        (void)hipFree(q.d_err);
         (void)hipFree(q.d_in);
         (void)hipFree(q.d_bits);
         (void)hipFree(q.d_valid);
@@ -73,6 +78,8 @@ static int stream_alloc(qpsk_stream* s) {
         SCHECK(hipMalloc((void**)&q.d_in, sizeof(int16_t) * cf * QK_FRAME));
         SCHECK(hipMalloc((void**)&q.d_bits, cf * QK_NBITS));
         SCHECK(hipMalloc((void**)&q.d_valid, cf));
+        SCHECK(hipMalloc((void**)&q.d_err, sizeof(int)));
+        SCHECK(hipHostMalloc((void**)&q.h_err, sizeof(int), hipHostMallocDefault));
         SCHECK(hipEventCreateWithFlags(&q.copied, hipEventDisableTiming));
         SCHECK(hipEventCreateWithFlags(&q.received, hipEventDisableTiming));
         SCHECK(hipEventCreateWithFlags(&q.done, hipEventDisableTiming));
@@ -153,13 +160,15 @@ extern "C" int qpsk_stream_submit(qpsk_stream* s) {
                           s->s_h2d));
     SCHECK(hipEventRecord(q.copied, s->s_h2d));
     SCHECK(hipStreamWaitEvent(s->s_rx, q.copied, 0));
-    const int r = qpsk_rx_batch_device(s->rx, q.d_in, s->frames, q.d_bits, q.d_valid, nullptr,
-                                       nullptr, s->s_rx);
+    SCHECK(hipMemsetAsync(q.d_err, 0, sizeof(int), s->s_rx));
+    const int r = qpsk_rx_launch(s->rx, q.d_in, s->frames, q.d_bits, q.d_valid, nullptr, nullptr,
+                                 s->s_rx, q.d_err);
     if (r != QPSK_OK) return r;
     SCHECK(hipEventRecord(q.received, s->s_rx));
     SCHECK(hipStreamWaitEvent(s->s_d2h, q.received, 0));
     SCHECK(hipMemcpyAsync(q.h_bits, q.d_bits, cf * QK_NBITS, hipMemcpyDeviceToHost, s->s_d2h));
     SCHECK(hipMemcpyAsync(q.h_valid, q.d_valid, cf, hipMemcpyDeviceToHost, s->s_d2h));
+    SCHECK(hipMemcpyAsync(q.h_err, q.d_err, sizeof(int), hipMemcpyDeviceToHost, s->s_d2h));
     SCHECK(hipEventRecord(q.done, s->s_d2h));
     s->submitted++;
     return QPSK_OK;
@@ -177,7 +186,9 @@ extern "C" int qpsk_stream_retrieve(qpsk_stream* s, const uint8_t** bits, const 
     *bits = q.h_bits;
     *valid = q.h_valid;
     s->retrieved++;
-    return QPSK_OK;
+    // a progress wait of this chunk's receive ran out: its bits are undefined
+    // (the slot is released all the same; the next chunks report their own)
+    return *q.h_err != 0 ? QPSK_ESTALL : QPSK_OK;
 }
 
 extern "C" qpsk_ctx* qpsk_stream_ctx(qpsk_stream* s) { return s ? s->rx : nullptr; }

@@ -286,11 +286,18 @@ def test_quad_back_exact_division(monkeypatch):
     _vs_oracle(x)
 
 
-def test_c4_shard_8192_channels():
-    """The C4 shard at N = 8 (8,192 channels x 32 frames, AWGN), as bench.py
-    --gpus 8 gives each rank, with the shape pick_shape selects (quad backs):
-    every output equals the oracle's."""
-    x = oracle.synth(81, 8192, 32, 6.0)
+@pytest.mark.parametrize("ngpu,c0", [(2, 32768), (4, 16384), (8, 57344)])
+def test_c4_shards_at_size(ngpu, c0):
+    """C4 (BASELINE configs[3]): the shard rank g of `bench.py --gpus N`
+    demodulates, at its stated size -- 65,536 / N channels x 32 frames, AWGN --
+    with the shape pick_shape selects for it (N = 2: 2x4 dual-chain, lane
+    backs; N = 4: 1x8 dual W = 64, lane backs, split 2; N = 8: 1x8 dual W = 32,
+    quad backs).  The shard's channels are the batch's channels
+    [c0, c0 + 65536 / N) (oracle.synth's channel offset): ranks 1, 1 and 7
+    of the three splits.  Every output, soft symbols included, equals the
+    oracle's (the loop being split is src/qpsk.c:436-458)."""
+    nch = 65536 // ngpu
+    x = oracle.synth(81, nch, 32, 6.0, c0=c0)
     _vs_oracle(x)
 
 

@@ -35,6 +35,38 @@ def test_stream_equals_one_batch(nslot):
     assert ev.any()
 
 
+def test_stream_reports_a_stalled_chunk(monkeypatch):
+    """A progress wait that runs out in a chunk's receive must come back from
+    qpsk_stream_retrieve() as QPSK_ESTALL for THAT chunk, never as bits with
+    QPSK_OK.  QPSK_DEBUG_STALL (read at creation) makes one wait of every call
+    unending on 96 channels (a dual-chain shape); the timeout is sticky per
+    workgroup, so the call ends after one bound.  A stream made without the
+    knob delivers the oracle's bits."""
+    nch, fpc = 96, 3
+    x = oracle.synth(18, nch, 2 * fpc, 6.0)
+    monkeypatch.setenv("QPSK_DEBUG_STALL", "1")
+    st = sc.Stream(nch, fpc, nslot=2)
+    monkeypatch.delenv("QPSK_DEBUG_STALL")
+    for k in range(2):
+        st.acquire()[...] = x[:, k * fpc:(k + 1) * fpc]
+        st.submit()
+    for _ in range(2):
+        with pytest.raises(sc.QpskError) as ei:
+            st.retrieve()
+        assert ei.value.code == sc.QPSK_ESTALL
+    assert st.pending == 0
+    st.close()
+    st = sc.Stream(nch, fpc, nslot=2)
+    got = []
+    for k in range(2):
+        st.acquire()[...] = x[:, k * fpc:(k + 1) * fpc]
+        st.submit()
+    while st.pending:
+        got.append(st.retrieve()[0])
+    st.close()
+    assert (np.concatenate(got, axis=1) == oracle.cpu_rx(x)[0]).all()
+
+
 def test_stream_busy_and_misuse():
     st = sc.Stream(64, 2, nslot=2)
     for _ in range(2):

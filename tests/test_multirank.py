@@ -79,10 +79,33 @@ def test_launcher_reports_a_failing_rank(tmp_path):
     assert bench.launch(2, [], script=str(script)) == 3
 
 
-def test_bench_gpus_flag_spawns_ranks(tmp_path):
-    """`bench.py --gpus 2` with no WORLD_SIZE re-runs itself as 2 ranks (here
-    only up to the parser: --help exits before any GPU work)."""
-    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK")}
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--help"],
-                       env=env, capture_output=True, text=True, timeout=120)
-    assert r.returncode == 0 and "--weak" in r.stdout
+def test_launcher_stops_the_peers_of_a_failed_rank(tmp_path):
+    """A rank that fails early must not leave its peers blocked (in gloo's
+    rendezvous, a barrier or a reduction) until a timeout: launch() watches
+    every child, terminates the rest and returns the failing status."""
+    import time
+    script = tmp_path / "hang.py"
+    script.write_text("import os, sys, time\n"
+                      "if os.environ['RANK'] == '1':\n    sys.exit(5)\n"
+                      "time.sleep(600)\n")
+    t = time.perf_counter()
+    assert bench.launch(3, [], script=str(script)) == 5
+    assert time.perf_counter() - t < 60
+
+
+def test_bench_gpus_flag_spawns_ranks():
+    """`bench.py --gpus 2` with no WORLD_SIZE runs itself as 2 ranks through
+    bench.launch(); --dry-run takes every rank through the host gloo group,
+    its C4 shard and the MAX/SUM reduction, and stops before any GPU call.
+    Rank 0's stdout is the one JSON line."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run"],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.strip().splitlines()
+    assert len(lines) == 1
+    out = json.loads(lines[0])
+    assert out["dry_run"] and out["world"] == 2 and out["channels_total"] == 65536
+    assert out["max_time_s"] == 0.002 and out["scaling"] == "strong"
+    assert out["shards"] == [{"rank": 0, "local_rank": 0, "channels": [0, 32768]},
+                             {"rank": 1, "local_rank": 1, "channels": [32768, 65536]}]
