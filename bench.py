@@ -162,6 +162,17 @@ def cpu_info() -> dict:
             "cpu_model": model, "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
 
 
+def host_cpus() -> int:
+    """CPUs this job may run on at once: the affinity set, capped by the cgroup
+    CPU quota (on the GPU boxes the affinity set is the node's 256 CPUs while
+    cpu.max grants 16: more workers than that only time-share them)."""
+    info = cpu_info()
+    n = info["affinity_cpus"] or os.cpu_count() or 1
+    if info["cgroup_cpu_quota"]:
+        n = min(n, max(1, int(info["cgroup_cpu_quota"])))
+    return n
+
+
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -190,9 +201,9 @@ def parse(argv=None):
                     help="C5: AWGN Eb/N0 sweep (GPU vs the reference C on host cores)")
     ap.add_argument("--sweep-frames", type=int, default=16)
     ap.add_argument("--sweep-points", type=str, default="0,1,2,3,4,5,6,7,8,9,10")
-    ap.add_argument("--cpu-procs", type=int, default=16,
-                    help="host processes for the multi-core reference baseline and the sweep "
-                         "(16 = one GPU's share of the box's host cores)")
+    ap.add_argument("--cpu-procs", type=int, default=0,
+                    help="host processes for the all-cores reference baseline and the sweep "
+                         "(0: every CPU this job may use, host_cpus())")
     ap.add_argument("--cpu-all-channels", type=int, default=32768,
                     help="channels of the multi-core reference sample (0: skip)")
     ap.add_argument("--dry-run", action="store_true",
@@ -400,6 +411,8 @@ def dry_run(args, world: int, rank: int, local: int, strong: bool) -> None:
 
 def main():
     args = parse()
+    if args.cpu_procs <= 0:
+        args.cpu_procs = host_cpus()
     if args.sweep:
         return sweep(args)
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -602,8 +615,9 @@ def main():
         cpu_all = {"value": round(tot / tmx / 1e6, 3), "unit": "Msamples/s",
                    "cores": len(jobs), "kind": "reference",
                    "sample": f"channels 0..{k - 1} of the {args.channels}-channel batch x {nf} "
-                             f"frames, {_ref_name(mode)}, {len(jobs)} host processes, "
-                             f"slowest {tmx:.1f} s", **host}
+                             f"frames, {_ref_name(mode)}, {len(jobs)} host processes (every CPU "
+                             f"this job may use: affinity {host['affinity_cpus']}, cgroup quota "
+                             f"{host['cgroup_cpu_quota']}), slowest {tmx:.1f} s", **host}
 
     if rank == 0:
         ch_total = total_ch

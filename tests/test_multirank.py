@@ -109,3 +109,16 @@ def test_bench_gpus_flag_spawns_ranks():
     assert out["max_time_s"] == 0.002 and out["scaling"] == "strong"
     assert out["shards"] == [{"rank": 0, "local_rank": 0, "channels": [0, 32768]},
                              {"rank": 1, "local_rank": 1, "channels": [32768, 65536]}]
+
+
+def test_host_cpus_honours_the_cgroup_quota(monkeypatch):
+    """The all-cores CPU baseline runs one reference process per CPU this job
+    may use: the affinity set, capped by the cgroup quota (the GPU boxes show
+    256 CPUs of affinity and a cpu.max of 16 CPUs)."""
+    base = {"nproc": 256, "cpu_model": "x", "omp_num_threads": None}
+    monkeypatch.setattr(bench, "cpu_info", lambda: {**base, "affinity_cpus": 256, "cgroup_cpu_quota": 16.0})
+    assert bench.host_cpus() == 16
+    monkeypatch.setattr(bench, "cpu_info", lambda: {**base, "affinity_cpus": 8, "cgroup_cpu_quota": None})
+    assert bench.host_cpus() == 8
+    monkeypatch.setattr(bench, "cpu_info", lambda: {**base, "affinity_cpus": 4, "cgroup_cpu_quota": 0.5})
+    assert bench.host_cpus() == 1
