@@ -819,6 +819,9 @@ struct Publish {
 
     __device__ __forceinline__ bool try_publish(bool valid) {
         if (lds_load(dseq) < n) return false;   // frame n-1 not published yet
+        // rt_n is read only after the counter showed it (the relaxed load
+        // alone would let the compiler hoist this read above it)
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
         *rt_next = valid ? mi + QK_NPRE : *rt_cur;   // src/qpsk.c:219
         // the rt word lands before the counter (same lane, LDS in order)
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
@@ -1394,6 +1397,19 @@ __global__ void __launch_bounds__(64 * (kBackWavesOf<G, FP, MODE, DUAL, W, QUAD>
     if (threadIdx.x == 0) dead_s = 0;
     __syncthreads();
     const bool back_on = (a.roles & 1) != 0, front_on = (a.roles & 2) != 0;   // QPSK_ABLATE
+    // front wave fl of group gi: its first channel within the group and how
+    // many of its channels are live.  roles bits 16-19 (split s, one group per
+    // workgroup only; pick_shape sets 2 at W = 64): the front waves that share
+    // a SIMD with a back wave (waves 4, 5, 8, 9 when waves map to SIMDs by
+    // wave % 4) take s channels fewer, the others s more
+    const int split = kGroups == 1 ? (a.roles >> 16) & 15 : 0;
+    auto share = [&](int x) { return ((x + kBackWaves) & 3) < kBackWaves; };
+    auto front_span = [&](int gi, int fl, int& cbeg) {
+        cbeg = 0;
+        for (int x = 0; x < fl; x++) cbeg += kFrontCh + (share(x) ? -split : split);
+        const int mych = kFrontCh + (share(fl) ? -split : split);
+        return front_on ? max(0, min(mych, a.nch - ((grp0 + gi) * W + cbeg))) : 0;
+    };
     if (wave < kBackWaves) {
         // -------------------------------------------------------------- back
         // wave = (group, sub-wave of the quad layout) x chain; chain w trains
@@ -1407,6 +1423,14 @@ __global__ void __launch_bounds__(64 * (kBackWavesOf<G, FP, MODE, DUAL, W, QUAD>
         const bool live = idx < W && ch < a.nch;
         const bool any = (grp0 + gi) * W < a.nch;     // a live channel in the group
         const bool lead = !QUAD || (lane & 3) == 0;   // the lane that publishes
+        // front waves of the group with a live channel: only they signal fcnt
+        // (a wave without channels would run through its frames at once and
+        // break the counters' two-frame bound)
+        int nfront = 0;
+        for (int fl = 0; fl < kFrontPer; fl++) {
+            int cb;
+            nfront += front_span(gi, fl, cb) > 0 ? 1 : 0;
+        }
         if (((a.roles >> 4) & 3) == 2) __builtin_amdgcn_s_setprio(2);
         // tests (roles bit kDebugStall): one wait that cannot end, on the
         // first back wave of workgroup 0, with a short bound
@@ -1417,8 +1441,8 @@ __global__ void __launch_bounds__(64 * (kBackWavesOf<G, FP, MODE, DUAL, W, QUAD>
         for (int n = chain; n < a.F; n += kChains) {
             const int p = n & 1;
             // every front of the group done with frame n-1: window n and mi_n
-            if (n > 0 && front_on)
-                spin_wait(&fcnt[gi][p ^ 1], kFrontPer * ((n - 1) / 2 + 1), a.err, &dead_s);
+            if (n > 0 && nfront > 0)
+                spin_wait(&fcnt[gi][p ^ 1], nfront * ((n - 1) / 2 + 1), a.err, &dead_s);
             STAMP(14);
             Publish pub{live && lead ? &dseq[gi][idx] : nullptr, &rt_s[gi][p][idx],
                         &rt_s[gi][p ^ 1][idx], n, mi_s[gi][p][idx], false};
@@ -1442,26 +1466,29 @@ __global__ void __launch_bounds__(64 * (kBackWavesOf<G, FP, MODE, DUAL, W, QUAD>
         const int f = wave - kBackWaves;
         const int gi = f / kFrontPer;
         const int fl = f % kFrontPer;
-        // roles bits 16-19 (split s, one group per workgroup only; pick_shape
-        // sets 2 at W = 64): the front waves that share a SIMD with a back
-        // wave (waves 4, 5, 8, 9 when waves map to SIMDs by wave % 4) take s
-        // channels fewer, the others s more
-        const int split = kGroups == 1 ? (a.roles >> 16) & 15 : 0;
-        auto share = [&](int x) { return ((x + kBackWaves) & 3) < kBackWaves; };
-        int cbeg = 0;
-        for (int x = 0; x < fl; x++) cbeg += kFrontCh + (share(x) ? -split : split);
-        const int mych = kFrontCh + (share(fl) ? -split : split);
+        int cbeg;
+        const int nlive = front_span(gi, fl, cbeg);
         const int ch0 = (grp0 + gi) * W + cbeg;
-        const int nlive = front_on ? max(0, min(mych, a.nch - ch0)) : 0;
         float2* M = Ms[f];
         int pf[kPf<DM>];
         if (((a.roles >> 4) & 3) == 1) __builtin_amdgcn_s_setprio(2);
+        // channel order within a frame: a channel whose decision of the
+        // previous frame is out goes before one still waiting for it (lane j
+        // looks at channel j; nlive <= 34)
+        const unsigned long long all = nlive > 0 ? (~0ull >> (64 - nlive)) : 0ull;
+        auto pick = [&](int m, unsigned long long todo) {
+            const bool ready = ((todo >> lane) & 1ull) != 0 &&
+                               (m == 0 || !back_on || lds_load(&dseq[gi][cbeg + min(lane, nlive - 1)]) >= m);
+            const unsigned long long r = __ballot(ready);
+            return __ffsll((long long)(r ? r : todo)) - 1;
+        };
+        int cur = 0;
         if (nlive > 0) prefetch<DM>(srcs(a, ch0, 0), lane, pf);
         // diagnostic stamps (QPSK_STAMPS): 0 mix, 1 window store + prefetch,
         // 8-12 front_channel phases (7: the wait for the channel's decision),
         // 6 its tail, 5 signal
         STAMP_DECL
-        for (int n = 0; n < a.F; n++) {
+        for (int n = 0; nlive > 0 && n < a.F; n++) {
             const int p = n & 1;
             const unsigned g = a.g0 + (unsigned)n;
             float2* wout = win_of(a, g + 1u);
@@ -1472,31 +1499,33 @@ __global__ void __launch_bounds__(64 * (kBackWavesOf<G, FP, MODE, DUAL, W, QUAD>
             if (!DUAL)
                 for (int z = (f >= kFrontWaves / 2) ? (a.roles >> 8) & 255 : 0; z > 0; z--)
                     __builtin_amdgcn_s_sleep(8);
-            int pmi = 0;
+            int pmi = 0, prv = 0;
+            unsigned long long todo = all;
             for (int c = 0; c < nlive; c++) {
-                const int ch = ch0 + c;
+                const int ch = ch0 + cur;
                 float2* dcur = decs[f][c % kDecBuf];
+                todo &= ~(1ull << cur);
                 mix<DM>(lane, pf, g, P, M);
                 STAMP(0);
-                if (c > 0) store_window(lane, pmi, decs[f][(c - 1) % kDecBuf], wout + (size_t)(ch - 1) * kWinStride);
-                {   // next channel of this frame, else the first of the next frame
-                    const bool same = c + 1 < nlive;
-                    if (same || n + 1 < a.F)
-                        prefetch<DM>(srcs(a, same ? ch + 1 : ch0, same ? n : n + 1), lane, pf);
-                }
+                if (c > 0) store_window(lane, pmi, decs[f][(c - 1) % kDecBuf], wout + (size_t)(ch0 + prv) * kWinStride);
+                // next channel of this frame, else the first of the next frame
+                const int nxt = todo ? pick(n, todo) : n + 1 < a.F ? pick(n + 1, all) : -1;
+                if (nxt >= 0) prefetch<DM>(srcs(a, ch0 + nxt, todo ? n : n + 1), lane, pf);
                 wave_lds_sync();
                 STAMP(1);
                 // rx_timing of frame n for this channel: frame n-1's decision
                 auto get_rt = [&] {
                     if (n > 0 && back_on)
-                        spin_wait<true>(&dseq[gi][cbeg + c], n, a.err, &dead_s);
-                    return rt_s[gi][p][cbeg + c];
+                        spin_wait<true>(&dseq[gi][cbeg + cur], n, a.err, &dead_s);
+                    return rt_s[gi][p][cbeg + cur];
                 };
                 pmi = front_channel<MODE>(lane, get_rt, M, dcur, BT FACC_ARG);
-                if (lane == 0) mi_s[gi][p ^ 1][cbeg + c] = pmi;
+                if (lane == 0) mi_s[gi][p ^ 1][cbeg + cur] = pmi;
                 if (c + 1 == nlive) store_window(lane, pmi, dcur, wout + (size_t)ch * kWinStride);
                 wave_lds_sync();
                 STAMP(6);
+                prv = cur;
+                cur = nxt;
             }
             signal_add(&fcnt[gi][p], 1, lane);
             STAMP(5);
@@ -1527,7 +1556,7 @@ float bits2f(uint32_t u) {
 
 // rx_kernel instantiations (pick_shape below)
 struct Shape {
-    enum Kind { k4x2, k2x4d, k1x8d16, k1x8d32, k1x8d64, k1x8q16, k1x8q32 };
+    enum Kind { k4x2, k2x4d, k1x8d16, k1x8d32, k1x8d64, k1x8q16, k1x8q32, k4x2d };
     int kind;
     int roles;
 };
@@ -1752,7 +1781,7 @@ extern "C" qpsk_ctx* qpsk_rx_create_mode(int device, int nch, int mode, int* err
         c->prio = !strcmp(pv, "none") ? 0 : !strcmp(pv, "front") ? 1 : !strcmp(pv, "back") ? 2 : -1;
     if (const char* sh = getenv("QPSK_SHAPE")) {
         c->shape = !strcmp(sh, "4x2") ? Shape::k4x2 : !strcmp(sh, "2x4d") ? Shape::k2x4d
-                 : !strcmp(sh, "1x8") ? Shape::k1x8d64 : -1;
+                 : !strcmp(sh, "1x8") ? Shape::k1x8d64 : !strcmp(sh, "4x2d") ? Shape::k4x2d : -1;
     }
     int r = herr(hipSetDevice(device));
     if (r == QPSK_OK) {
@@ -1891,6 +1920,7 @@ int qpsk_rx_launch(qpsk_ctx* c, const int16_t* d_in, int F, uint8_t* d_bits, uin
             case Shape::k1x8d64: QPSK_LAUNCH(1, 8, MM, true, 64, false); break;                \
             case Shape::k1x8q16: QPSK_LAUNCH(1, 8, MM, true, 16, true); break;                 \
             case Shape::k1x8q32: QPSK_LAUNCH(1, 8, MM, true, 32, true); break;                 \
+            case Shape::k4x2d: QPSK_LAUNCH(4, 2, MM, true, 64, false); break;                  \
             default: QPSK_LAUNCH(4, 2, MM, false, 64, false); break;                           \
         }                                                                                      \
     } while (0)
