@@ -6,7 +6,7 @@
 #   bash profiles/r03_call.sh N [tests|bench|prof|env]...
 set -u
 N=$1; shift
-O=gpurun_out/c${N}
+O=gpurun_out/r3c${N}
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 check() { # name rc

@@ -88,8 +88,8 @@ struct RxArgs {
     int16_t* hist;           // [nch][2][1880]: frames -2, -1 of this call
     const float2* ptab;      // [1880] mixer table P[t] * 2^-14
     const unsigned long long* ks;  // [1057] keystream bits of frame g (mod 1057)
-    float2* win;             // [4][nslot][168] equalizer windows, by global frame mod 4
-    size_t wstride;          // nslot * 168: one ring buffer
+    float2* win0;            // [nslot][168] equalizer windows, even global frames
+    float2* win1;            //                                odd global frames
     int* mi0;                // [nslot] preamble position (even / odd frames)
     int* mi1;
     int* rt0;                // [nslot] rx_timing (even / odd frames)
@@ -130,11 +130,7 @@ __device__ __forceinline__ unsigned long long stamp_now() {
 #define STAMP_FLUSH() do { } while (0)
 #endif
 
-// Window of global frame g.  Four buffers: with early decisions (below) the
-// front of frame n writes window n+1 while the back of frame n-1 may still read
-// window n-1, and window n+1 reuses the buffer of window n-3, whose back ended
-// before the back of frame n-1 began (same wave, or the single back wave).
-__device__ __forceinline__ float2* win_of(const RxArgs& a, unsigned g) { return a.win + (size_t)(g & 3u) * a.wstride; }
+__device__ __forceinline__ float2* win_of(const RxArgs& a, unsigned g) { return (g & 1u) ? a.win1 : a.win0; }
 __device__ __forceinline__ int* mi_of(const RxArgs& a, unsigned g) { return (g & 1u) ? a.mi1 : a.mi0; }
 __device__ __forceinline__ int* rt_of(const RxArgs& a, unsigned g) { return (g & 1u) ? a.rt1 : a.rt0; }
 
@@ -144,45 +140,35 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Progress between the waves of a workgroup goes through LDS counters, not
-// workgroup barriers (rx_kernel: fcnt, the fronts' frames; dseq, the
-// per-channel decisions).  Every wave of the (single) workgroup is resident,
-// and every counter is advanced by every frame of its producer, so each wait
-// ends.  The bound keeps a logic error from hanging the GPU: a wait that runs
-// out sets kErrStall in the call's device error word, which the host returns
-// as QPSK_ESTALL (qpsk_rx_sync / qpsk_rx_batch / qpsk_stream_retrieve), so
-// stale windows or rx_timing never pass as a result.  The timeout is sticky per
-// workgroup: it also sets the LDS word `dead`, and every later wait of the
-// workgroup returns at once, so a broken counter costs one bound per
-// workgroup, not one per frame.
+// Dual-chain kernel (rx_kernel<.., DUAL = true>): per-frame progress counters
+// in LDS instead of a workgroup barrier.  Every wave of the (single) workgroup
+// is resident, and every counter is advanced by every frame of its producer,
+// so each wait ends.  The bound keeps a logic error from hanging the GPU: a
+// wait that runs out sets kErrStall in the call's device error word, which
+// the host returns as QPSK_ESTALL (qpsk_rx_sync / qpsk_rx_batch /
+// qpsk_stream_retrieve), so stale windows or rx_timing never pass as a result.
+// The timeout is sticky per workgroup: it also sets the LDS word `dead`, and
+// every later wait of the workgroup returns at once, so a broken counter costs
+// one bound per workgroup, not one per frame.
 constexpr unsigned kSpinBound = 1u << 22;   // ~0.1 s; a frame is ~2.5k spins
 constexpr int kErrStall = 1;                // device error word bits
 
-__device__ __forceinline__ int lds_load(const int* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-__device__ __forceinline__ void stall(int* err, int* dead) {
-    __hip_atomic_store(dead, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    atomicOr(err, kErrStall);
-}
-
-// wave-uniform wait for *p >= v.  LDS_ONLY: what the counter hands over is in
-// LDS only (the acquire then waits for LDS operations, never for this wave's
-// outstanding global loads); otherwise global stores of the producer too.
-template <bool LDS_ONLY = false>
 __device__ __forceinline__ void spin_wait(int* p, int v, int* err, int* dead,
                                           unsigned bound = kSpinBound) {
     unsigned it = 0;
     for (; it < bound; it++) {
-        const int c = __builtin_amdgcn_readfirstlane(lds_load(p));
-        const int d = __builtin_amdgcn_readfirstlane(lds_load(dead));
+        const int c = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+        const int d = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_load(dead, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
         if (c >= v || d != 0) break;
         __builtin_amdgcn_s_sleep(1);
     }
-    if (it == bound && __lane_id() == 0) stall(err, dead);
-    if (LDS_ONLY) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-    else __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    if (it == bound && __lane_id() == 0) {
+        __hip_atomic_store(dead, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        atomicOr(err, kErrStall);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
 // publish: every earlier store of this wave (LDS and global) is visible to the
@@ -495,29 +481,23 @@ __device__ __forceinline__ int hunt(int lane, float2* M, const float2* dec, cons
 }
 
 // One channel of frame n's front: D_n (decimated with rx_timing rt), F_{n+1},
-// correlation of dec_{n+1} = [D_n, F_{n+1}] and its argmax mi.  F_{n+1} does
-// not depend on rx_timing, so it runs before get_rt(), which may wait for the
-// channel's decision of frame n-1.
-template <int MODE, typename RtFn>
-__device__ __forceinline__ int front_channel(int lane, RtFn get_rt, float2* M, float2* dec,
+// correlation of dec_{n+1} = [D_n, F_{n+1}] and its argmax mi.
+template <int MODE>
+__device__ __forceinline__ int front_channel(int lane, int rt, float2* M, float2* dec,
                                              const float* BT FACC_PARAM) {
 #ifdef QPSK_STAMPS
     unsigned long long ft0 = stamp_now();
 #endif
     if constexpr ((MODE & 1) != 0) {
-        const int rt = get_rt();
-        FSTAMP(7 - 8);
         fir_dec752(lane, rt, M, dec);
         FSTAMP(0);
     } else {
-        fir_head(lane, M, dec);
-        FSTAMP(1);
-        const int rt = get_rt();
-        FSTAMP(7 - 8);
         fir_dec(lane, rt, M, dec);
         FSTAMP(0);
+        fir_head(lane, M, dec);
     }
     wave_lds_sync();
+    FSTAMP(1);
     return hunt<MODE>(lane, M, dec, BT FACC_FWD);
 }
 
@@ -790,119 +770,52 @@ __device__ __forceinline__ void load_x0(const float4* wp, f2 (&x)[5]) {
 constexpr int kForceExact = 64;   // roles bit: take the exact-division path (tests)
 constexpr int kDebugStall = 128;  // roles bit: force one progress wait past its bound (tests)
 
-// ---------------------------------------------------------------- decisions
-// Early decisions.  Frame n+1's front needs only rx_timing of frame n+1, i.e.
-// frame n's decision (src/qpsk.c:196-219): valid_n ? mi_n + 128 : rt_n.  valid_n
-// is matches > 98 over the 128 train_eq steps, and matches only grows, so the
-// decision is certain before the training ends: once matches > 98 (valid),
-// or once 30 steps have missed (matches <= 98 whatever follows).  A back lane
-// checks that every 4 steps and publishes its channel's rt_{n+1} at once; the
-// front of frame n+1 starts on that channel while the training of frame n
-// goes on (its remaining steps still give the state the data symbols
-// continue from, and the trace's full count).  On the oracle's C3 workload
-// the channels decide at step 78 (invalid) and 108 (valid) in the median.
-//
-// Per channel, dseq[ch] = frames of the call whose decision is published;
-// rt_s[n & 1][ch] = rt_n.  Frame n publishes only after frame n-1 has (dseq ==
-// n), so rt_{n+1} never overwrites rt_{n-1} before frame n-1's readers are
-// done: the front of frame n-1 read it before frame n's window existed, and the
-// back of frame n-1 before publishing.  An invalid frame needs rt_n itself,
-// which is that same condition.  A lane publishes early only while no lane of
-// its wave has left the fast reciprocal's range (`bad`): the steps up to then
-// are exact, and the exact recompute of the frame reaches the same decision.
-struct Publish {
-    int* dseq;          // the lane's channel counter in LDS; null: nothing to publish
-    const int* rt_cur;  // rt_s[n & 1][ch]
-    int* rt_next;       // rt_s[(n + 1) & 1][ch]
-    int n, mi;
-    bool done;
-
-    __device__ __forceinline__ bool try_publish(bool valid) {
-        if (lds_load(dseq) < n) return false;   // frame n-1 not published yet
-        // rt_n is read only after the counter showed it (the relaxed load
-        // alone would let the compiler hoist this read above it)
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-        *rt_next = valid ? mi + QK_NPRE : *rt_cur;   // src/qpsk.c:219
-        // the rt word lands before the counter (same lane, LDS in order)
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-        __hip_atomic_store(dseq, n + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        done = true;
-        return true;
-    }
-    // after `steps` training steps with `matches` so far
-    __device__ __forceinline__ void operator()(int matches, int steps, bool bad) {
-        const bool want = dseq != nullptr && !done &&
-                          (matches > QK_MATCH_MIN || steps - matches >= QK_NPRE - QK_MATCH_MIN);
-        if (__ballot(want) == 0ull || __ballot(bad) != 0ull) return;   // wave-uniform
-        if (want) try_publish(matches > QK_MATCH_MIN);
-    }
-    // after the training: every lane that has not published waits for frame
-    // n-1's decision of its channel and publishes (bounded, lane-wise)
-    __device__ __forceinline__ void finish(bool valid, int* err, int* dead) {
-        bool need = dseq != nullptr && !done;
-        for (unsigned it = 0; __ballot(need) != 0ull; it++) {
-            if (need && try_publish(valid)) need = false;
-            if (__ballot(need) == 0ull) break;
-            if (it == kSpinBound || __builtin_amdgcn_readfirstlane(lds_load(dead)) != 0) {
-                if (__lane_id() == 0 && it == kSpinBound) stall(err, dead);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-    }
-};
-
 // 128 x train_eq (src/equalizer.c:45-58) from the window; returns matches.
-// Every 4 steps `pub` may publish the frame's decision early (Publish).
 // (The window load one step ahead stays: a 4-step ring loaded an iteration
 // ahead, as qtrain's, changes this loop's schedule to one with ~50 s_nop per
 // step in the 4x2 kernel.)
 template <bool EXACT>
-__device__ __forceinline__ int train(Kal& k, f2 (&x)[5], const f2* wp2, bool& bad, Publish& pub) {
+__device__ __forceinline__ int train(Kal& k, f2 (&x)[5], const f2* wp2, bool& bad) {
     int matches = 0;
-    for (int i0 = 0; i0 < QK_NPRE; i0 += 4) {
+#pragma unroll 4
+    for (int i = 0; i < QK_NPRE; i++) {
+        const f2 nx = wp2[i + 6];                  // slot i+6 (next step)
+        const unsigned long long m = i < 64 ? kPreLo : kPreHi;
+        const float ref = ((m >> (i & 63)) & 1ull) ? 1.0f : -1.0f;
+        f2 v = {0.0f, 0.0f};
 #pragma unroll
-        for (int t = 0; t < 4; t++) {
-            const int i = i0 + t;
-            const f2 nx = wp2[i + 6];                  // slot i+6 (next step)
-            const unsigned long long m = i < 64 ? kPreLo : kPreHi;
-            const float ref = ((m >> (i & 63)) & 1ull) ? 1.0f : -1.0f;
-            f2 v = {0.0f, 0.0f};
+        for (int t = 0; t < 5; t++) v = v + cmul(x[t], k.eq[t]);
+        const float er = ref - v.x;                // conjf(ref - val) = (ref - vr, vi)
+        update_eq<EXACT>(k, x, f2{er, v.y}, bad);
+        if (er * ref > 0.0f) matches++;
 #pragma unroll
-            for (int tt = 0; tt < 5; tt++) v = v + cmul(x[tt], k.eq[tt]);
-            const float er = ref - v.x;                // conjf(ref - val) = (ref - vr, vi)
-            update_eq<EXACT>(k, x, f2{er, v.y}, bad);
-            if (er * ref > 0.0f) matches++;
-#pragma unroll
-            for (int tt = 0; tt < 4; tt++) x[tt] = x[tt + 1];
-            x[4] = nx;
-        }
-        pub(matches, i0 + 4, bad);
+        for (int t = 0; t < 4; t++) x[t] = x[t + 1];
+        x[4] = nx;
     }
     return matches;
 }
 
 // One frame of the back wave: lane = channel.  Window slots 1..163 hold
-// dec[mi .. mi+162]; read two slots (16 B) every two steps.  The frame's
-// decision goes out through `pub` (early when certain, else after training).
-__device__ __forceinline__ void back_frame(const RxArgs& a, int ch, bool live, int n, Publish& pub,
-                                           const float2* win, int* dead) {
+// dec[mi .. mi+162]; read two slots (16 B) every two steps.
+// get_rt() yields rx_timing of frame n; it is called only after the training,
+// so the dual-chain kernel can wait for the previous frame's decision there.
+template <typename RtFn>
+__device__ __forceinline__ void back_frame(const RxArgs& a, int ch, bool live, int n, int mi,
+                                           RtFn get_rt, const float2* win, int* rt_next) {
     const float4* wp = reinterpret_cast<const float4*>(win);
-    const int mi = pub.mi;
     Kal k = kal_reset();
     f2 x[5];
     load_x0(wp, x);
     // equalize(): 128 x train_eq (src/qpsk.c:111-123, src/equalizer.c:45-58)
     const f2* wp2 = reinterpret_cast<const f2*>(win);
     bool bad = (a.roles & kForceExact) != 0;
-    int matches = train<false>(k, x, wp2, bad, pub);
+    int matches = train<false>(k, x, wp2, bad);
     if (__builtin_expect(__ballot(bad) != 0ull, 0)) {   // recompute the frame exactly
         k = kal_reset();
         load_x0(wp, x);
-        matches = train<true>(k, x, wp2, bad, pub);
+        matches = train<true>(k, x, wp2, bad);
     }
     const bool valid = live && matches > QK_MATCH_MIN;   // src/qpsk.c:196
-    pub.finish(valid, a.err, dead);
     const size_t cf = (size_t)ch * a.F + n;
     // Valid frames continue in rx_data_kernel (data_eq needs nothing the next
     // frame depends on): enqueue the equalizer state and the 35 window samples
@@ -929,10 +842,13 @@ __device__ __forceinline__ void back_frame(const RxArgs& a, int ch, bool live, i
             for (int ss = 0; ss < QK_NDSYM; ss++) so[ss] = make_float2(0.0f, 0.0f);
         }
     }
+    const int rt = get_rt();
+    const int rtn = valid ? mi + QK_NPRE : rt;    // src/qpsk.c:219
+    *rt_next = rtn;
     if (live) {
         a.valid[cf] = valid ? 1 : 0;
         if (a.trace)
-            *reinterpret_cast<int4*>(a.trace + cf * 4) = make_int4(mi, matches, valid ? 1 : 0, *pub.rt_next);
+            *reinterpret_cast<int4*>(a.trace + cf * 4) = make_int4(mi, matches, valid ? 1 : 0, rtn);
     }
 }
 
@@ -1105,8 +1021,7 @@ __device__ __forceinline__ void qload_x0(const f2* wp2, int c, f2 (&X)[5]) {
 // L2 round trip every step.  wl[s] = x[c+1] of step s; the reads run to step
 // 135, inside the 168-slot window row.
 template <bool EXACT>
-__device__ __forceinline__ int qtrain(QKal& k, f2 (&X)[5], const f2* wl, int c, bool& bad,
-                                     Publish& pub) {
+__device__ __forceinline__ int qtrain(QKal& k, f2 (&X)[5], const f2* wl, int c, bool& bad) {
     int matches = 0;
     f2 B[4];
 #pragma unroll
@@ -1128,32 +1043,29 @@ __device__ __forceinline__ int qtrain(QKal& k, f2 (&X)[5], const f2* wl, int c, 
         }
 #pragma unroll
         for (int t = 0; t < 4; t++) B[t] = Bn[t];
-        pub(matches, i + 4, bad);
     }
     return matches;
 }
 
 // back_frame() for a quad per channel: every lane of the quad has the same
-// matches / valid / rt; the quad's lane 0 publishes and writes the per-channel
-// outputs.
-__device__ __forceinline__ void back_frame_quad(const RxArgs& a, int ch, bool live, int n,
-                                                Publish& pub, const float2* win, int* dead) {
+// matches / valid / rt; the quad's lane 0 writes the per-channel outputs.
+template <typename RtFn>
+__device__ __forceinline__ void back_frame_quad(const RxArgs& a, int ch, bool live, int n, int mi,
+                                                RtFn get_rt, const float2* win, int* rt_next) {
     const int c = lane_id() & 3;
     const bool lead = c == 0;
-    const int mi = pub.mi;
     const f2* wp2 = reinterpret_cast<const f2*>(win);
     QKal k = qkal_reset();
     f2 X[5];
     qload_x0(wp2, c, X);
     bool bad = (a.roles & kForceExact) != 0;
-    int matches = qtrain<false>(k, X, wp2 + c + 2, c, bad, pub);
+    int matches = qtrain<false>(k, X, wp2 + c + 2, c, bad);
     if (__builtin_expect(__ballot(bad) != 0ull, 0)) {   // recompute the frame exactly
         k = qkal_reset();
         qload_x0(wp2, c, X);
-        matches = qtrain<true>(k, X, wp2 + c + 2, c, bad, pub);
+        matches = qtrain<true>(k, X, wp2 + c + 2, c, bad);
     }
     const bool valid = live && matches > QK_MATCH_MIN;   // src/qpsk.c:196
-    pub.finish(valid, a.err, dead);
     const size_t cf = (size_t)ch * a.F + n;
     const unsigned long long vm = __ballot(valid && lead);
     if (vm) {   // gather the quad's state (all lanes take part in the DPP moves)
@@ -1194,10 +1106,13 @@ __device__ __forceinline__ void back_frame_quad(const RxArgs& a, int ch, bool li
             for (int ss = c; ss < QK_NDSYM; ss += 4) so[ss] = make_float2(0.0f, 0.0f);
         }
     }
+    const int rt = get_rt();
+    const int rtn = valid ? mi + QK_NPRE : rt;    // src/qpsk.c:219
+    if (lead) *rt_next = rtn;
     if (live && lead) {
         a.valid[cf] = valid ? 1 : 0;
         if (a.trace)
-            *reinterpret_cast<int4*>(a.trace + cf * 4) = make_int4(mi, matches, valid ? 1 : 0, *pub.rt_next);
+            *reinterpret_cast<int4*>(a.trace + cf * 4) = make_int4(mi, matches, valid ? 1 : 0, rtn);
     }
 }
 
@@ -1310,27 +1225,15 @@ __global__ void __launch_bounds__(256) rx_data_kernel(const float4* jobs, unsign
 // the argument block is indexed dynamically (no scratch copy).
 // 12 waves per workgroup, 3 per SIMD (<= 168 VGPRs), one workgroup per CU (LDS).
 //
-// Waves hand progress over through LDS counters, never a workgroup barrier
-// inside the frame loop:
-//   fcnt[g][p]  front frames of parity p finished, summed over the group's
-//               front waves (windows and mi of the next frame are out);
-//   dseq[g][ch] frames of the call whose decision (rx_timing of the next
-//               frame) is published for the channel (Publish).
-// A front waits per channel for the decision it needs, so frame n+1's front
-// runs while frame n's training finishes; a back waits for the whole group's
-// fronts of the previous frame (its windows).  Fronts stay within two frames
-// of each other: a front of frame n+1 needs a decision of frame n, and the back
-// of frame n started only after every front of frame n-1 was done, which is
-// what makes the parity counters exact.
-//
 // DUAL (G <= 2): two back waves per group, one for the even and one for the odd
 // frames of the call.  Frame n's training needs only frame n-1's front, and
 // frame n-1's front needs frame n-2's decision, so consecutive frames' training
 // is independent: the back of frame n+1 starts as soon as the front of frame n
 // is done, while the back of frame n is still running.  The per-frame time
 // drops from max(back, front) to (back + front) / 2 where one serial back wave
-// per CU bounds the kernel (<= 16,384 channels per GPU).  Without DUAL one back
-// wave per group trains every frame (C3's 4x2).
+// per CU bounds the kernel (<= 16,384 channels per GPU).  Progress is handed
+// over through LDS counters (bseq: frames decided per back wave; fcnt: front
+// frames finished, by frame parity) instead of __syncthreads().
 //
 // W (DUAL only): channels per group, 64, 32 or 16.  A narrower group leaves
 // back lanes idle but spreads a small batch over more CUs and gives each front
@@ -1339,25 +1242,24 @@ __global__ void __launch_bounds__(256) rx_data_kernel(const float4* jobs, unsign
 // QUAD (DUAL, G == 1 only): the back waves hold a quad of lanes per channel
 // (back_frame_quad), 16 channels per wave, W / 16 waves per frame chain.
 template <int G, int FP, int MODE, bool DUAL, int W, bool QUAD>
-constexpr int kBackWavesOf = (DUAL ? 2 : 1) * G * (QUAD ? W / 16 : 1);
+constexpr int kBackWavesOf = DUAL ? 2 * G * (QUAD ? W / 16 : 1) : G;
 
 template <int G, int FP, int MODE, bool DUAL, int W = QK_GROUP, bool QUAD = false>
 __global__ void __launch_bounds__(64 * (kBackWavesOf<G, FP, MODE, DUAL, W, QUAD> + G * FP), 3) rx_kernel(
     const int16_t* in, int16_t* hist, const float2* ptab, const unsigned long long* ks,
-    float2* win, unsigned long long wstride, int* mi0, int* mi1, int* rt0, int* rt1, uint8_t* bits,
+    float2* win0, float2* win1, int* mi0, int* mi1, int* rt0, int* rt1, uint8_t* bits,
     uint8_t* valid, int32_t* trace, float2* soft, float4* jobs, unsigned* njobs, int nch, int F,
     unsigned g0, int roles, const float* fft_tab, unsigned long long jcap, int* err) {
     static_assert(W == QK_GROUP || (DUAL && G == 1 && W % FP == 0 && W <= QK_GROUP), "group width");
     static_assert(!QUAD || (DUAL && G == 1 && W % 16 == 0), "quad backs: dual chain, one group");
     constexpr int kGroups = G, kFrontPer = FP;
-    constexpr int kChains = DUAL ? 2 : 1;              // back waves per group and channel
-    constexpr int kChainWaves = QUAD ? W / 16 : 1;     // back waves per frame chain and group
     constexpr int kBackWaves = kBackWavesOf<G, FP, MODE, DUAL, W, QUAD>;
+    constexpr int kChainWaves = QUAD ? W / 16 : 1;     // back waves per frame chain and group
     constexpr int kFrontCh = W / kFrontPer;            // channels per front wave
     constexpr int kFrontWaves = kGroups * kFrontPer;
     constexpr int kBlock = 64 * (kBackWaves + kFrontWaves);
-    const RxArgs a{in, hist, ptab, ks, win, (size_t)wstride, mi0, mi1, rt0, rt1, bits, valid, trace,
-                   soft, jobs, njobs, nch, F, g0, (size_t)jcap, roles, err};
+    const RxArgs a{in, hist, ptab, ks, win0, win1, mi0, mi1, rt0, rt1, bits, valid, trace, soft,
+                   jobs, njobs, nch, F, g0, (size_t)jcap, roles, err};
     __shared__ __attribute__((aligned(16))) float2 P[QK_FRAME];
     constexpr int DM = MODE & 1;   // decimation semantics; MODE & 2: FFT hunt
     constexpr int kM = Cfg<DM>::kM, kDecBuf = Cfg<DM>::kDecBuf;
@@ -1366,9 +1268,8 @@ __global__ void __launch_bounds__(64 * (kBackWavesOf<G, FP, MODE, DUAL, W, QUAD>
     __shared__ int mi_s[kGroups][2][QK_GROUP], rt_s[kGroups][2][QK_GROUP];
     // hunt tables: the MFMA correlator's B, or the FFT hunt's twiddles / Q / permutation
     __shared__ __attribute__((aligned(16))) float BT[(MODE & 2) ? kFftHT : kHuntTab];
-    __shared__ int dseq[kGroups][QK_GROUP];   // decisions published, per channel
-    __shared__ int fcnt[kGroups][2];          // front frames finished, by parity
-    __shared__ int dead_s;                    // a wait of this workgroup timed out
+    __shared__ int bseq[kGroups][2], fcnt[kGroups][2];   // DUAL progress counters, per group
+    __shared__ int dead_s;                               // DUAL: a wait of this workgroup timed out
     const int lane = threadIdx.x & 63;
     // wave-uniform by construction; readfirstlane tells the compiler, so every
     // per-wave index and pointer below lives in SGPRs
@@ -1391,156 +1292,200 @@ __global__ void __launch_bounds__(64 * (kBackWavesOf<G, FP, MODE, DUAL, W, QUAD>
             mi_s[wave][0][lane] = mi_of(a, a.g0)[ch];
             rt_s[wave][0][lane] = rt_of(a, a.g0)[ch];
         }
-        dseq[wave][lane] = 0;
     }
-    if (threadIdx.x < 2 * kGroups) (&fcnt[0][0])[threadIdx.x] = 0;
+    if (threadIdx.x < 2 * kGroups) (&bseq[0][0])[threadIdx.x] = (&fcnt[0][0])[threadIdx.x] = 0;
     if (threadIdx.x == 0) dead_s = 0;
     __syncthreads();
-    const bool back_on = (a.roles & 1) != 0, front_on = (a.roles & 2) != 0;   // QPSK_ABLATE
-    // front wave fl of group gi: its first channel within the group and how
-    // many of its channels are live.  roles bits 16-19 (split s, one group per
-    // workgroup only; pick_shape sets 2 at W = 64): the front waves that share
-    // a SIMD with a back wave (waves 4, 5, 8, 9 when waves map to SIMDs by
-    // wave % 4) take s channels fewer, the others s more
-    const int split = kGroups == 1 ? (a.roles >> 16) & 15 : 0;
-    auto share = [&](int x) { return ((x + kBackWaves) & 3) < kBackWaves; };
-    auto front_span = [&](int gi, int fl, int& cbeg) {
-        cbeg = 0;
-        for (int x = 0; x < fl; x++) cbeg += kFrontCh + (share(x) ? -split : split);
-        const int mych = kFrontCh + (share(fl) ? -split : split);
-        return front_on ? max(0, min(mych, a.nch - ((grp0 + gi) * W + cbeg))) : 0;
-    };
-    if (wave < kBackWaves) {
-        // -------------------------------------------------------------- back
-        // wave = (group, sub-wave of the quad layout) x chain; chain w trains
-        // the frames n = w mod kChains
-        const int chain = wave % kChains;
-        const int rest = wave / kChains;
-        const int gi = rest / kChainWaves;
-        // channel of this lane within the group: the lane, or its quad
-        const int idx = QUAD ? 16 * (rest % kChainWaves) + (lane >> 2) : lane;
-        const int ch = (grp0 + gi) * W + idx;
-        const bool live = idx < W && ch < a.nch;
-        const bool any = (grp0 + gi) * W < a.nch;     // a live channel in the group
-        const bool lead = !QUAD || (lane & 3) == 0;   // the lane that publishes
-        // front waves of the group with a live channel: only they signal fcnt
-        // (a wave without channels would run through its frames at once and
-        // break the counters' two-frame bound)
-        int nfront = 0;
-        for (int fl = 0; fl < kFrontPer; fl++) {
-            int cb;
-            nfront += front_span(gi, fl, cb) > 0 ? 1 : 0;
-        }
-        if (((a.roles >> 4) & 3) == 2) __builtin_amdgcn_s_setprio(2);
-        // tests (roles bit kDebugStall): one wait that cannot end, on the
-        // first back wave of workgroup 0, with a short bound
-        if ((a.roles & kDebugStall) && blockIdx.x == 0 && wave == 0)
-            spin_wait(&fcnt[gi][0], 1 << 30, a.err, &dead_s, 1u << 12);
-        // diagnostic stamps (QPSK_STAMPS): 13 frame work, 14 wait for the fronts
-        STAMP_DECL
-        for (int n = chain; n < a.F; n += kChains) {
-            const int p = n & 1;
-            // every front of the group done with frame n-1: window n and mi_n
-            if (n > 0 && nfront > 0)
-                spin_wait(&fcnt[gi][p ^ 1], nfront * ((n - 1) / 2 + 1), a.err, &dead_s);
-            STAMP(14);
-            Publish pub{live && lead ? &dseq[gi][idx] : nullptr, &rt_s[gi][p][idx],
-                        &rt_s[gi][p ^ 1][idx], n, mi_s[gi][p][idx], false};
-            if (back_on && any) {
+    if constexpr (DUAL) {
+        // bseq[gi][p]: frames of parity p decided, summed over the chain's back
+        // waves; frame m is decided by all of them once it reaches this
+        auto decided = [](int m) { return kChainWaves * (m / 2 + 1); };
+        if (wave < kBackWaves) {
+            // ---------------------------------------------------- back of group
+            // (wave >> 1) / kChainWaves, frames n = wave mod 2
+            const int gi = (wave >> 1) / kChainWaves;
+            // channel of this lane within the group: the lane, or its quad
+            const int idx = QUAD ? 16 * ((wave >> 1) % kChainWaves) + (lane >> 2) : lane;
+            const int ch = (grp0 + gi) * W + idx;
+            const bool live = idx < W && ch < a.nch;
+            if (((a.roles >> 4) & 3) == 2) __builtin_amdgcn_s_setprio(2);
+            // tests (roles bit kDebugStall): one wait that cannot end, on the
+            // first back wave of workgroup 0, with a short bound
+            if ((a.roles & kDebugStall) && blockIdx.x == 0 && wave == 0)
+                spin_wait(&fcnt[gi][0], 1 << 30, a.err, &dead_s, 1u << 12);
+            // diagnostic stamps (QPSK_STAMPS): 13 frame work, 14 wait for the
+            // fronts, 15 wait for the other chain's decision
+            STAMP_DECL
+            for (int n = wave & 1; n < a.F; n += 2) {
+                const int p = n & 1;
+                // front(n-1) done by every front wave of the group: window n and mi_n
+                if (n > 0) spin_wait(&fcnt[gi][p ^ 1], kFrontPer * ((n - 1) / 2 + 1), a.err, &dead_s);
+                STAMP(14);
+                const int mi = mi_s[gi][p][idx];
+                auto get_rt = [&] {   // rx_timing of frame n = the decision of frame n-1
+                    STAMP(13);
+                    if (n > 0) spin_wait(&bseq[gi][p ^ 1], decided(n - 1), a.err, &dead_s);
+                    STAMP(15);
+                    return rt_s[gi][p][idx];
+                };
                 const float2* wn = win_of(a, a.g0 + (unsigned)n) + (size_t)(live ? ch : 0) * kWinStride;
                 if constexpr (QUAD)
-                    back_frame_quad(a, live ? ch : 0, live, n, pub, wn, &dead_s);
+                    back_frame_quad(a, live ? ch : 0, live, n, mi, get_rt, wn, &rt_s[gi][p ^ 1][idx]);
                 else
-                    back_frame(a, live ? ch : 0, live, n, pub, wn, &dead_s);
-            } else {
-                pub.finish(false, a.err, &dead_s);   // ablation: rx_timing carries over
+                    back_frame(a, live ? ch : 0, live, n, mi, get_rt, wn, &rt_s[gi][p ^ 1][idx]);
+                signal_add(&bseq[gi][p], 1, lane);
+                STAMP(13);
             }
+            STAMP_FLUSH();
+        } else {
+            // ---------------------------------------------------- front
+            const int f = wave - kBackWaves;
+            const int gi = f / kFrontPer;
+            const int fl = f % kFrontPer;
+            // roles bits 16-19 (split s, one group per workgroup only; pick_shape
+            // sets 2 at W = 64): the front waves that share a SIMD with a back
+            // wave (waves 4, 5, 8, 9 when waves map to SIMDs by wave % 4) take s
+            // channels fewer, the others s more
+            const int split = kGroups == 1 ? (a.roles >> 16) & 15 : 0;
+            auto share = [&](int x) { return ((x + kBackWaves) & 3) < kBackWaves; };
+            int cbeg = 0;
+            for (int x = 0; x < fl; x++) cbeg += kFrontCh + (share(x) ? -split : split);
+            const int mych = kFrontCh + (share(fl) ? -split : split);
+            const int ch0 = (grp0 + gi) * W + cbeg;
+            const int nlive = max(0, min(mych, a.nch - ch0));
+            float2* M = Ms[f];
+            int pf[kPf<DM>];
+            if (((a.roles >> 4) & 3) == 1) __builtin_amdgcn_s_setprio(2);
+            if (nlive > 0) prefetch<DM>(srcs(a, ch0, 0), lane, pf);
+            // diagnostic stamps (QPSK_STAMPS): 7 wait for the backs, 0 mix,
+            // 1 window store + prefetch, 8-12 front_channel phases, 6 its tail,
+            // 5 signal
+            STAMP_DECL
+            for (int n = 0; n < a.F; n++) {
+                const int p = n & 1;
+                const unsigned g = a.g0 + (unsigned)n;
+                float2* wout = win_of(a, g + 1u);
+                // back(n-1) done: rx_timing of frame n, and window n+1's buffer
+                // (window n-1) and mi_s[p ^ 1] (mi_{n-1}) are free
+                if (n > 0) spin_wait(&bseq[gi][p ^ 1], decided(n - 1), a.err, &dead_s);
+                STAMP(7);
+                int pmi = 0;
+                for (int c = 0; c < nlive; c++) {
+                    const int ch = ch0 + c;
+                    float2* dcur = decs[f][c % kDecBuf];
+                    mix<DM>(lane, pf, g, P, M);
+                    STAMP(0);
+                    if (c > 0) store_window(lane, pmi, decs[f][(c - 1) % kDecBuf], wout + (size_t)(ch - 1) * kWinStride);
+                    {
+                        const bool same = c + 1 < nlive;
+                        if (same || n + 1 < a.F)
+                            prefetch<DM>(srcs(a, same ? ch + 1 : ch0, same ? n : n + 1), lane, pf);
+                    }
+                    wave_lds_sync();
+                    STAMP(1);
+                    pmi = front_channel<MODE>(lane, rt_s[gi][p][cbeg + c], M, dcur, BT FACC_ARG);
+                    if (lane == 0) mi_s[gi][p ^ 1][cbeg + c] = pmi;
+                    if (c + 1 == nlive) store_window(lane, pmi, dcur, wout + (size_t)ch * kWinStride);
+                    wave_lds_sync();
+                    STAMP(6);
+                }
+                signal_add(&fcnt[gi][p], 1, lane);
+                STAMP(5);
+            }
+            STAMP_FLUSH();
+            carry_history<DM>(a.in, a.hist, a.F, ch0, nlive, lane);
+        }
+        __syncthreads();
+        if (wave < kBackWaves && (wave & 1) == 0) {   // state after the call's last frame
+            const int gi = (wave >> 1) / kChainWaves;
+            const int idx = QUAD ? 16 * ((wave >> 1) % kChainWaves) + (lane >> 2) : lane;
+            const int ch = (grp0 + gi) * W + idx;
+            if (idx < W && ch < a.nch && (!QUAD || (lane & 3) == 0)) {
+                const unsigned ge = a.g0 + (unsigned)a.F;
+                mi_of(a, ge)[ch] = mi_s[gi][a.F & 1][idx];
+                rt_of(a, ge)[ch] = rt_s[gi][a.F & 1][idx];
+            }
+        }
+        return;
+    }
+    if (wave < kGroups) {
+        // ------------------------------------------------------------ back
+        const int gi = wave;
+        const int ch = (grp0 + gi) * QK_GROUP + lane;
+        const bool live = ch < a.nch;
+        const bool any = (grp0 + gi) * QK_GROUP < a.nch;
+        if (((a.roles >> 4) & 3) == 2) __builtin_amdgcn_s_setprio(2);
+        STAMP_DECL
+        for (int n = 0; n < a.F; n++) {
+            const int p = n & 1;
+            if (any && (a.roles & 1)) {
+                const int rt = rt_s[gi][p][lane];
+                back_frame(a, live ? ch : 0, live, n, mi_s[gi][p][lane], [=] { return rt; },
+                           win_of(a, a.g0 + (unsigned)n) + (size_t)(live ? ch : 0) * kWinStride,
+                           &rt_s[gi][p ^ 1][lane]);
+            }
+            else
+                rt_s[gi][p ^ 1][lane] = rt_s[gi][p][lane];
             STAMP(13);
+            __syncthreads();
+            STAMP(14);
         }
         STAMP_FLUSH();
+        if (live) {   // per-channel state after the call's last frame
+            const unsigned ge = a.g0 + (unsigned)a.F;
+            mi_of(a, ge)[ch] = mi_s[gi][a.F & 1][lane];
+            rt_of(a, ge)[ch] = rt_s[gi][a.F & 1][lane];
+        }
     } else {
-        // ------------------------------------------------------------- front
+        // ------------------------------------------------------------ front
         // channel by channel: mix (prefetched samples) -> store the previous
-        // channel's window -> prefetch the next channel -> [FIR head] -> wait
-        // for the channel's rx_timing -> FIR decimation -> hunt -> window
-        const int f = wave - kBackWaves;
+        // channel's window -> prefetch the next channel -> FIR/correlate/argmax
+        const int f = wave - kGroups;
         const int gi = f / kFrontPer;
-        const int fl = f % kFrontPer;
-        int cbeg;
-        const int nlive = front_span(gi, fl, cbeg);
-        const int ch0 = (grp0 + gi) * W + cbeg;
+        const int cbeg = (f % kFrontPer) * kFrontCh;
+        const int ch0 = (grp0 + gi) * QK_GROUP + cbeg;
+        const int nlive = max(0, min(kFrontCh, a.nch - ch0));
         float2* M = Ms[f];
         int pf[kPf<DM>];
+        const bool on = (a.roles & 2) != 0 && nlive > 0;
         if (((a.roles >> 4) & 3) == 1) __builtin_amdgcn_s_setprio(2);
-        // channel order within a frame: a channel whose decision of the
-        // previous frame is out goes before one still waiting for it (lane j
-        // looks at channel j; nlive <= 34)
-        const unsigned long long all = nlive > 0 ? (~0ull >> (64 - nlive)) : 0ull;
-        auto pick = [&](int m, unsigned long long todo) {
-            const bool ready = ((todo >> lane) & 1ull) != 0 &&
-                               (m == 0 || !back_on || lds_load(&dseq[gi][cbeg + min(lane, nlive - 1)]) >= m);
-            const unsigned long long r = __ballot(ready);
-            return __ffsll((long long)(r ? r : todo)) - 1;
-        };
-        int cur = 0;
-        if (nlive > 0) prefetch<DM>(srcs(a, ch0, 0), lane, pf);
-        // diagnostic stamps (QPSK_STAMPS): 0 mix, 1 window store + prefetch,
-        // 8-12 front_channel phases (7: the wait for the channel's decision),
-        // 6 its tail, 5 signal
+        if (on) prefetch<DM>(srcs(a, ch0, 0), lane, pf);
         STAMP_DECL
-        for (int n = 0; nlive > 0 && n < a.F; n++) {
+        for (int n = 0; n < a.F; n++) {
             const int p = n & 1;
             const unsigned g = a.g0 + (unsigned)n;
             float2* wout = win_of(a, g + 1u);
-            // roles bits 8-15 (stagger, 4x2 only): the second half of the front
-            // waves (the younger partner on each SIMD) starts each frame that
-            // many x 512 cycles late, so partners' FIR and MFMA/LDS phases
-            // interleave (MI355X_MICROARCH.md "two waves per SIMD", item 9)
-            if (!DUAL)
-                for (int z = (f >= kFrontWaves / 2) ? (a.roles >> 8) & 255 : 0; z > 0; z--)
-                    __builtin_amdgcn_s_sleep(8);
-            int pmi = 0, prv = 0;
-            unsigned long long todo = all;
-            for (int c = 0; c < nlive; c++) {
-                const int ch = ch0 + cur;
+            int pmi = 0;
+            // roles bits 8-15 (stagger, kStagger): the second half of the front waves
+            // (the younger partner on each SIMD) starts each frame that many x
+            // 512 cycles late, so partners' FIR and MFMA/LDS phases interleave
+            // (MI355X_MICROARCH.md "two waves per SIMD", item 9)
+            for (int z = (f >= kFrontWaves / 2) ? (a.roles >> 8) & 255 : 0; z > 0; z--)
+                __builtin_amdgcn_s_sleep(8);
+            for (int c = 0; on && c < nlive; c++) {
+                const int ch = ch0 + c;
                 float2* dcur = decs[f][c % kDecBuf];
-                todo &= ~(1ull << cur);
                 mix<DM>(lane, pf, g, P, M);
                 STAMP(0);
-                if (c > 0) store_window(lane, pmi, decs[f][(c - 1) % kDecBuf], wout + (size_t)(ch0 + prv) * kWinStride);
-                // next channel of this frame, else the first of the next frame
-                const int nxt = todo ? pick(n, todo) : n + 1 < a.F ? pick(n + 1, all) : -1;
-                if (nxt >= 0) prefetch<DM>(srcs(a, ch0 + nxt, todo ? n : n + 1), lane, pf);
+                if (c > 0) store_window(lane, pmi, decs[f][(c - 1) % kDecBuf], wout + (size_t)(ch - 1) * kWinStride);
+                {   // next channel of this frame, else the first of the next frame
+                    const bool same = c + 1 < nlive;
+                    if (same || n + 1 < a.F)
+                        prefetch<DM>(srcs(a, same ? ch + 1 : ch0, same ? n : n + 1), lane, pf);
+                }
                 wave_lds_sync();
                 STAMP(1);
-                // rx_timing of frame n for this channel: frame n-1's decision
-                auto get_rt = [&] {
-                    if (n > 0 && back_on)
-                        spin_wait<true>(&dseq[gi][cbeg + cur], n, a.err, &dead_s);
-                    return rt_s[gi][p][cbeg + cur];
-                };
-                pmi = front_channel<MODE>(lane, get_rt, M, dcur, BT FACC_ARG);
-                if (lane == 0) mi_s[gi][p ^ 1][cbeg + cur] = pmi;
+                pmi = front_channel<MODE>(lane, rt_s[gi][p][cbeg + c], M, dcur, BT FACC_ARG);
+                if (lane == 0) mi_s[gi][p ^ 1][cbeg + c] = pmi;
                 if (c + 1 == nlive) store_window(lane, pmi, dcur, wout + (size_t)ch * kWinStride);
                 wave_lds_sync();
                 STAMP(6);
-                prv = cur;
-                cur = nxt;
             }
-            signal_add(&fcnt[gi][p], 1, lane);
-            STAMP(5);
+            __syncthreads();
+            STAMP(7);
         }
         STAMP_FLUSH();
         carry_history<DM>(a.in, a.hist, a.F, ch0, nlive, lane);
-    }
-    __syncthreads();
-    if (wave < kGroups) {   // state after the call's last frame
-        const int ch = (grp0 + wave) * W + lane;
-        if (lane < W && ch < a.nch) {
-            const unsigned ge = a.g0 + (unsigned)a.F;
-            mi_of(a, ge)[ch] = mi_s[wave][a.F & 1][lane];
-            rt_of(a, ge)[ch] = rt_s[wave][a.F & 1][lane];
-        }
     }
 }
 
@@ -1556,7 +1501,7 @@ float bits2f(uint32_t u) {
 
 // rx_kernel instantiations (pick_shape below)
 struct Shape {
-    enum Kind { k4x2, k2x4d, k1x8d16, k1x8d32, k1x8d64, k1x8q16, k1x8q32, k4x2d };
+    enum Kind { k4x2, k2x4d, k1x8d16, k1x8d32, k1x8d64, k1x8q16, k1x8q32 };
     int kind;
     int roles;
 };
@@ -1575,7 +1520,7 @@ struct qpsk_ctx {
     float2* d_ptab = nullptr;
     unsigned long long* d_ks = nullptr;
     int16_t* d_hist = nullptr;
-    float2* d_win = nullptr;      // [4][nslot][168] equalizer windows, by global frame mod 4
+    float2* d_win[2] = {nullptr, nullptr};
     int* d_mi[2] = {nullptr, nullptr};
     int* d_rt[2] = {nullptr, nullptr};
     // data-symbol jobs of valid frames (rx_kernel -> rx_data_kernel)
@@ -1658,8 +1603,8 @@ static int ctx_alloc(qpsk_ctx* c) {
     HCHECK(hipMalloc(&c->d_njobs, sizeof(unsigned) * 2));
     HCHECK(hipMalloc(&c->d_err, 2 * sizeof(int)));
     HCHECK(hipEventCreateWithFlags(&c->done, hipEventDisableTiming));
-    HCHECK(hipMalloc(&c->d_win, sizeof(float2) * 4 * nslot(c) * kWinStride));
     for (int p = 0; p < 2; p++) {
+        HCHECK(hipMalloc(&c->d_win[p], sizeof(float2) * nslot(c) * kWinStride));
         HCHECK(hipMalloc(&c->d_mi[p], sizeof(int) * nslot(c)));
         HCHECK(hipMalloc(&c->d_rt[p], sizeof(int) * nslot(c)));
     }
@@ -1673,8 +1618,8 @@ extern "C" int qpsk_rx_reset(qpsk_ctx* c) {
     HCHECK(hipMemsetAsync(c->d_hist, 0, sizeof(int16_t) * ns * 2 * QK_FRAME, c->stream));
     HCHECK(hipMemsetAsync(c->d_njobs, 0, sizeof(unsigned) * 2, c->stream));
     HCHECK(hipMemsetAsync(c->d_err, 0, 2 * sizeof(int), c->stream));
-    HCHECK(hipMemsetAsync(c->d_win, 0, sizeof(float2) * 4 * ns * kWinStride, c->stream));
     for (int p = 0; p < 2; p++) {
+        HCHECK(hipMemsetAsync(c->d_win[p], 0, sizeof(float2) * ns * kWinStride, c->stream));
         HCHECK(hipMemsetAsync(c->d_mi[p], 0, sizeof(int) * ns, c->stream));
     }
     int* rt0 = (int*)malloc(sizeof(int) * ns);
@@ -1702,8 +1647,8 @@ static void ctx_free(qpsk_ctx* c) {
     (void)hipFree(c->d_ks);
     (void)hipFree(c->d_hist);
     (void)hipFree(c->d_fft);
-    (void)hipFree(c->d_win);
     for (int p = 0; p < 2; p++) {
+        (void)hipFree(c->d_win[p]);
         (void)hipFree(c->d_mi[p]);
         (void)hipFree(c->d_rt[p]);
     }
@@ -1781,7 +1726,7 @@ extern "C" qpsk_ctx* qpsk_rx_create_mode(int device, int nch, int mode, int* err
         c->prio = !strcmp(pv, "none") ? 0 : !strcmp(pv, "front") ? 1 : !strcmp(pv, "back") ? 2 : -1;
     if (const char* sh = getenv("QPSK_SHAPE")) {
         c->shape = !strcmp(sh, "4x2") ? Shape::k4x2 : !strcmp(sh, "2x4d") ? Shape::k2x4d
-                 : !strcmp(sh, "1x8") ? Shape::k1x8d64 : !strcmp(sh, "4x2d") ? Shape::k4x2d : -1;
+                 : !strcmp(sh, "1x8") ? Shape::k1x8d64 : -1;
     }
     int r = herr(hipSetDevice(device));
     if (r == QPSK_OK) {
@@ -1905,8 +1850,7 @@ int qpsk_rx_launch(qpsk_ctx* c, const int16_t* d_in, int F, uint8_t* d_bits, uin
                        dim3((unsigned)((c->nch + (size_t)GG * WW - 1) / ((size_t)GG * WW))),   \
                        dim3(64 * (kBackWavesOf<GG, FF, MM, DD, WW, QQ> + GG * FF)), 0, s,      \
                        d_in, c->d_hist, c->d_ptab,                                             \
-                       c->d_ks, c->d_win, (unsigned long long)(nslot(c) * kWinStride),         \
-                       c->d_mi[0], c->d_mi[1], c->d_rt[0],                                     \
+                       c->d_ks, c->d_win[0], c->d_win[1], c->d_mi[0], c->d_mi[1], c->d_rt[0],  \
                        c->d_rt[1], d_bits, d_valid, d_trace, reinterpret_cast<float2*>(d_soft), \
                        c->d_jobs, c->d_njobs + parity, c->nch, F,                               \
                        (unsigned)(c->frames & 0xffffffffu), sh.roles, c->d_fft,                \
@@ -1920,7 +1864,6 @@ int qpsk_rx_launch(qpsk_ctx* c, const int16_t* d_in, int F, uint8_t* d_bits, uin
             case Shape::k1x8d64: QPSK_LAUNCH(1, 8, MM, true, 64, false); break;                \
             case Shape::k1x8q16: QPSK_LAUNCH(1, 8, MM, true, 16, true); break;                 \
             case Shape::k1x8q32: QPSK_LAUNCH(1, 8, MM, true, 32, true); break;                 \
-            case Shape::k4x2d: QPSK_LAUNCH(4, 2, MM, true, 64, false); break;                  \
             default: QPSK_LAUNCH(4, 2, MM, false, 64, false); break;                           \
         }                                                                                      \
     } while (0)
