@@ -844,7 +844,7 @@ __device__ __forceinline__ void back_frame(const RxArgs& a, int ch, bool live, i
     }
     const int rt = get_rt();
     const int rtn = valid ? mi + QK_NPRE : rt;    // src/qpsk.c:219
-    *rt_next = rtn;
+    if (rt_next) *rt_next = rtn;   // null: a lane past its block (no channel)
     if (live) {
         a.valid[cf] = valid ? 1 : 0;
         if (a.trace)
@@ -1268,7 +1268,9 @@ __global__ void __launch_bounds__(64 * (kBackWavesOf<G, FP, MODE, DUAL, W, QUAD>
     __shared__ int mi_s[kGroups][2][QK_GROUP], rt_s[kGroups][2][QK_GROUP];
     // hunt tables: the MFMA correlator's B, or the FFT hunt's twiddles / Q / permutation
     __shared__ __attribute__((aligned(16))) float BT[(MODE & 2) ? kFftHT : kHuntTab];
-    __shared__ int bseq[kGroups][2], fcnt[kGroups][2];   // DUAL progress counters, per group
+    // DUAL progress counters, per group, frame parity and channel block (one
+    // block per back wave of a chain)
+    __shared__ int bseq[kGroups][2][kChainWaves], fcnt[kGroups][2][kChainWaves];
     __shared__ int dead_s;                               // DUAL: a wait of this workgroup timed out
     const int lane = threadIdx.x & 63;
     // wave-uniform by construction; readfirstlane tells the compiler, so every
@@ -1293,47 +1295,64 @@ __global__ void __launch_bounds__(64 * (kBackWavesOf<G, FP, MODE, DUAL, W, QUAD>
             rt_s[wave][0][lane] = rt_of(a, a.g0)[ch];
         }
     }
-    if (threadIdx.x < 2 * kGroups) (&bseq[0][0])[threadIdx.x] = (&fcnt[0][0])[threadIdx.x] = 0;
+    if (threadIdx.x < 2 * kGroups * kChainWaves) (&bseq[0][0][0])[threadIdx.x] = (&fcnt[0][0][0])[threadIdx.x] = 0;
     if (threadIdx.x == 0) dead_s = 0;
     __syncthreads();
     if constexpr (DUAL) {
-        // bseq[gi][p]: frames of parity p decided, summed over the chain's back
-        // waves; frame m is decided by all of them once it reaches this
-        auto decided = [](int m) { return kChainWaves * (m / 2 + 1); };
+        // Channel blocks: a group's channels split into one block per back wave
+        // of a chain (QUAD: 16 channels; lane backs: the whole group).  A back
+        // wave waits only for the fronts of its own block, and the front waves
+        // serve the blocks one at a time (every front wave takes its share of
+        // block 0, signals, then block 1): a block's windows are ready after
+        // its share of the front work, not the group's, and the chain waves
+        // settle into a stagger of one block's front time
+        // (profiles/r03_blocks_ab.txt; lane backs split into 32-channel blocks
+        // were measured too: slower, two back waves issue every step).
+        // bseq[gi][p][b]: frames of parity p decided by block b's back wave;
+        // fcnt[gi][p][b]: front waves done with block b of parity-p frames.
+        constexpr int kBlkCh = W / kChainWaves;            // channels per block
+        constexpr int kFrontChB = kBlkCh / kFrontPer;      // per front wave and block
+        static_assert(kBlkCh % kFrontPer == 0, "block split");
         if (wave < kBackWaves) {
             // ---------------------------------------------------- back of group
-            // (wave >> 1) / kChainWaves, frames n = wave mod 2
+            // gi = (wave >> 1) / kChainWaves, block b, frames n = wave mod 2
             const int gi = (wave >> 1) / kChainWaves;
-            // channel of this lane within the group: the lane, or its quad
-            const int idx = QUAD ? 16 * ((wave >> 1) % kChainWaves) + (lane >> 2) : lane;
+            const int b = (wave >> 1) % kChainWaves;
+            // channel of this lane within the block: the lane, or its quad.
+            // Lanes past the block (lane backs with W < 64) own no channel:
+            // they read their block's first channel's slots and write none.
+            const int sub = QUAD ? lane >> 2 : lane;
+            const bool own = sub < kBlkCh;
+            const int idx = kBlkCh * b + (own ? sub : 0);
             const int ch = (grp0 + gi) * W + idx;
-            const bool live = idx < W && ch < a.nch;
+            const bool live = own && ch < a.nch;
             if (((a.roles >> 4) & 3) == 2) __builtin_amdgcn_s_setprio(2);
             // tests (roles bit kDebugStall): one wait that cannot end, on the
             // first back wave of workgroup 0, with a short bound
             if ((a.roles & kDebugStall) && blockIdx.x == 0 && wave == 0)
-                spin_wait(&fcnt[gi][0], 1 << 30, a.err, &dead_s, 1u << 12);
+                spin_wait(&fcnt[gi][0][0], 1 << 30, a.err, &dead_s, 1u << 12);
             // diagnostic stamps (QPSK_STAMPS): 13 frame work, 14 wait for the
             // fronts, 15 wait for the other chain's decision
             STAMP_DECL
             for (int n = wave & 1; n < a.F; n += 2) {
                 const int p = n & 1;
-                // front(n-1) done by every front wave of the group: window n and mi_n
-                if (n > 0) spin_wait(&fcnt[gi][p ^ 1], kFrontPer * ((n - 1) / 2 + 1), a.err, &dead_s);
+                // front(n-1) done by every front wave for this block: window n and mi_n
+                if (n > 0) spin_wait(&fcnt[gi][p ^ 1][b], kFrontPer * ((n - 1) / 2 + 1), a.err, &dead_s);
                 STAMP(14);
                 const int mi = mi_s[gi][p][idx];
                 auto get_rt = [&] {   // rx_timing of frame n = the decision of frame n-1
                     STAMP(13);
-                    if (n > 0) spin_wait(&bseq[gi][p ^ 1], decided(n - 1), a.err, &dead_s);
+                    if (n > 0) spin_wait(&bseq[gi][p ^ 1][b], (n - 1) / 2 + 1, a.err, &dead_s);
                     STAMP(15);
                     return rt_s[gi][p][idx];
                 };
                 const float2* wn = win_of(a, a.g0 + (unsigned)n) + (size_t)(live ? ch : 0) * kWinStride;
+                int* rtn = own ? &rt_s[gi][p ^ 1][idx] : nullptr;
                 if constexpr (QUAD)
-                    back_frame_quad(a, live ? ch : 0, live, n, mi, get_rt, wn, &rt_s[gi][p ^ 1][idx]);
+                    back_frame_quad(a, live ? ch : 0, live, n, mi, get_rt, wn, rtn);
                 else
-                    back_frame(a, live ? ch : 0, live, n, mi, get_rt, wn, &rt_s[gi][p ^ 1][idx]);
-                signal_add(&bseq[gi][p], 1, lane);
+                    back_frame(a, live ? ch : 0, live, n, mi, get_rt, wn, rtn);
+                signal_add(&bseq[gi][p][b], 1, lane);
                 STAMP(13);
             }
             STAMP_FLUSH();
@@ -1342,65 +1361,78 @@ __global__ void __launch_bounds__(64 * (kBackWavesOf<G, FP, MODE, DUAL, W, QUAD>
             const int f = wave - kBackWaves;
             const int gi = f / kFrontPer;
             const int fl = f % kFrontPer;
-            // roles bits 16-19 (split s, one group per workgroup only; pick_shape
-            // sets 2 at W = 64): the front waves that share a SIMD with a back
-            // wave (waves 4, 5, 8, 9 when waves map to SIMDs by wave % 4) take s
-            // channels fewer, the others s more
-            const int split = kGroups == 1 ? (a.roles >> 16) & 15 : 0;
+            // roles bits 16-19 (split s, one group and one block per workgroup
+            // only; pick_shape sets 2 at W = 64): the front waves that share a
+            // SIMD with a back wave (waves 4, 5, 8, 9 when waves map to SIMDs by
+            // wave % 4) take s channels fewer, the others s more
+            const int split = (kGroups == 1 && kChainWaves == 1) ? (a.roles >> 16) & 15 : 0;
             auto share = [&](int x) { return ((x + kBackWaves) & 3) < kBackWaves; };
             int cbeg = 0;
-            for (int x = 0; x < fl; x++) cbeg += kFrontCh + (share(x) ? -split : split);
-            const int mych = kFrontCh + (share(fl) ? -split : split);
-            const int ch0 = (grp0 + gi) * W + cbeg;
-            const int nlive = max(0, min(mych, a.nch - ch0));
+            for (int x = 0; x < fl; x++) cbeg += kFrontChB + (share(x) ? -split : split);
+            const int mych = kFrontChB + (share(fl) ? -split : split);
+            // this wave's channels of block bb: group index kBlkCh * bb + cbeg + c
+            auto bch0 = [&](int bb) { return (grp0 + gi) * W + kBlkCh * bb + cbeg; };
+            auto blive = [&](int bb) { return max(0, min(mych, a.nch - bch0(bb))); };
             float2* M = Ms[f];
             int pf[kPf<DM>];
             if (((a.roles >> 4) & 3) == 1) __builtin_amdgcn_s_setprio(2);
-            if (nlive > 0) prefetch<DM>(srcs(a, ch0, 0), lane, pf);
+            if (blive(0) > 0) prefetch<DM>(srcs(a, bch0(0), 0), lane, pf);
             // diagnostic stamps (QPSK_STAMPS): 7 wait for the backs, 0 mix,
             // 1 window store + prefetch, 8-12 front_channel phases, 6 its tail,
             // 5 signal
             STAMP_DECL
+            int k = 0;   // channels done, for the dec buffer ring
             for (int n = 0; n < a.F; n++) {
                 const int p = n & 1;
                 const unsigned g = a.g0 + (unsigned)n;
                 float2* wout = win_of(a, g + 1u);
-                // back(n-1) done: rx_timing of frame n, and window n+1's buffer
-                // (window n-1) and mi_s[p ^ 1] (mi_{n-1}) are free
-                if (n > 0) spin_wait(&bseq[gi][p ^ 1], decided(n - 1), a.err, &dead_s);
-                STAMP(7);
-                int pmi = 0;
-                for (int c = 0; c < nlive; c++) {
-                    const int ch = ch0 + c;
-                    float2* dcur = decs[f][c % kDecBuf];
-                    mix<DM>(lane, pf, g, P, M);
-                    STAMP(0);
-                    if (c > 0) store_window(lane, pmi, decs[f][(c - 1) % kDecBuf], wout + (size_t)(ch - 1) * kWinStride);
-                    {
-                        const bool same = c + 1 < nlive;
-                        if (same || n + 1 < a.F)
-                            prefetch<DM>(srcs(a, same ? ch + 1 : ch0, same ? n : n + 1), lane, pf);
+                for (int bb = 0; bb < kChainWaves; bb++) {
+                    // back(n-1) of this block done: rx_timing of frame n, and
+                    // window n+1's buffer (window n-1) and mi_{n-1} are free
+                    if (n > 0) spin_wait(&bseq[gi][p ^ 1][bb], (n - 1) / 2 + 1, a.err, &dead_s);
+                    STAMP(7);
+                    const int c0 = bch0(bb), nl = blive(bb);
+                    const int i0 = kBlkCh * bb + cbeg;
+                    int pmi = 0;
+                    for (int c = 0; c < nl; c++, k++) {
+                        const int ch = c0 + c;
+                        float2* dcur = decs[f][k % kDecBuf];
+                        mix<DM>(lane, pf, g, P, M);
+                        STAMP(0);
+                        if (c > 0) store_window(lane, pmi, decs[f][(k - 1) % kDecBuf], wout + (size_t)(ch - 1) * kWinStride);
+                        {   // the next channel: of this block, the next live block, or frame n+1
+                            int nb = bb, nc = c + 1, nn = n;
+                            if (nc >= nl) {
+                                nc = 0;
+                                nb = bb + 1;
+                                while (nb < kChainWaves && blive(nb) == 0) nb++;
+                                if (nb == kChainWaves) { nb = 0; nn = n + 1; }
+                            }
+                            if (nn < a.F) prefetch<DM>(srcs(a, bch0(nb) + nc, nn), lane, pf);
+                        }
+                        wave_lds_sync();
+                        STAMP(1);
+                        pmi = front_channel<MODE>(lane, rt_s[gi][p][i0 + c], M, dcur, BT FACC_ARG);
+                        if (lane == 0) mi_s[gi][p ^ 1][i0 + c] = pmi;
+                        if (c + 1 == nl) store_window(lane, pmi, dcur, wout + (size_t)ch * kWinStride);
+                        wave_lds_sync();
+                        STAMP(6);
                     }
-                    wave_lds_sync();
-                    STAMP(1);
-                    pmi = front_channel<MODE>(lane, rt_s[gi][p][cbeg + c], M, dcur, BT FACC_ARG);
-                    if (lane == 0) mi_s[gi][p ^ 1][cbeg + c] = pmi;
-                    if (c + 1 == nlive) store_window(lane, pmi, dcur, wout + (size_t)ch * kWinStride);
-                    wave_lds_sync();
-                    STAMP(6);
+                    signal_add(&fcnt[gi][p][bb], 1, lane);
+                    STAMP(5);
                 }
-                signal_add(&fcnt[gi][p], 1, lane);
-                STAMP(5);
             }
             STAMP_FLUSH();
-            carry_history<DM>(a.in, a.hist, a.F, ch0, nlive, lane);
+            for (int bb = 0; bb < kChainWaves; bb++)
+                carry_history<DM>(a.in, a.hist, a.F, bch0(bb), blive(bb), lane);
         }
         __syncthreads();
         if (wave < kBackWaves && (wave & 1) == 0) {   // state after the call's last frame
             const int gi = (wave >> 1) / kChainWaves;
-            const int idx = QUAD ? 16 * ((wave >> 1) % kChainWaves) + (lane >> 2) : lane;
+            const int sub = QUAD ? lane >> 2 : lane;
+            const int idx = kBlkCh * ((wave >> 1) % kChainWaves) + sub;
             const int ch = (grp0 + gi) * W + idx;
-            if (idx < W && ch < a.nch && (!QUAD || (lane & 3) == 0)) {
+            if (sub < kBlkCh && ch < a.nch && (!QUAD || (lane & 3) == 0)) {
                 const unsigned ge = a.g0 + (unsigned)a.F;
                 mi_of(a, ge)[ch] = mi_s[gi][a.F & 1][idx];
                 rt_of(a, ge)[ch] = rt_s[gi][a.F & 1][idx];
@@ -1858,12 +1890,12 @@ int qpsk_rx_launch(qpsk_ctx* c, const int16_t* d_in, int F, uint8_t* d_bits, uin
 #define QPSK_LAUNCH_MODE(MM)                                                                   \
     do {                                                                                       \
         switch (sh.kind) {                                                                     \
-            case Shape::k2x4d: QPSK_LAUNCH(2, 4, MM, true, 64, false); break;                  \
-            case Shape::k1x8d16: QPSK_LAUNCH(1, 8, MM, true, 16, false); break;                \
-            case Shape::k1x8d32: QPSK_LAUNCH(1, 8, MM, true, 32, false); break;                \
-            case Shape::k1x8d64: QPSK_LAUNCH(1, 8, MM, true, 64, false); break;                \
-            case Shape::k1x8q16: QPSK_LAUNCH(1, 8, MM, true, 16, true); break;                 \
-            case Shape::k1x8q32: QPSK_LAUNCH(1, 8, MM, true, 32, true); break;                 \
+            case Shape::k2x4d: QPSK_LAUNCH(2, 4, MM, true, 64, false); break;              \
+            case Shape::k1x8d16: QPSK_LAUNCH(1, 8, MM, true, 16, false); break;            \
+            case Shape::k1x8d32: QPSK_LAUNCH(1, 8, MM, true, 32, false); break;            \
+            case Shape::k1x8d64: QPSK_LAUNCH(1, 8, MM, true, 64, false); break;            \
+            case Shape::k1x8q16: QPSK_LAUNCH(1, 8, MM, true, 16, true); break;             \
+            case Shape::k1x8q32: QPSK_LAUNCH(1, 8, MM, true, 32, true); break;             \
             default: QPSK_LAUNCH(4, 2, MM, false, 64, false); break;                           \
         }                                                                                      \
     } while (0)
