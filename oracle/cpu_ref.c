@@ -267,6 +267,8 @@ static int data_eq(kal_t *k, const float (*x)[2], float soft[2]) {
 static int rx_frame(qc_chan_t *ch, const int16_t in[QC_FRAME], uint8_t bits[QC_BITS],
                     qc_trace_t *tr, float (*dec_out)[2]);
 
+int qc_decision_step;
+
 int qc_rx_frame(qc_chan_t *ch, const int16_t in[QC_FRAME], uint8_t bits[QC_BITS],
                 qc_trace_t *tr) {
     return rx_frame(ch, in, bits, tr, NULL);
@@ -351,10 +353,14 @@ static int rx_frame(qc_chan_t *ch, const int16_t in[QC_FRAME], uint8_t bits[QC_B
     kal_t k;
     kal_reset(&k);
     int matches = 0;
+    int dstep = QC_PRE;
     for (int i = 0; i < QC_PRE; i++) {
         float ref = (float)k_pre[i];
         if (train_eq(&k, dec + mi + i, ref) * ref > 0.0f) matches++;
+        /* diagnostics: first step at which the decision below is certain */
+        if (dstep == QC_PRE && (matches > QC_PRE - 30 || i + 1 - matches >= 30)) dstep = i + 1;
     }
+    qc_decision_step = dstep;
     const int valid = matches > QC_PRE - 30;  /* src/qpsk.c:196 */
     memset(bits, 0, QC_BITS);
     if (tr) memset(tr, 0, sizeof(*tr));

@@ -1,7 +1,9 @@
+/* Block decision steps of the bench workload (profiles/r03_early_decision_ab.txt):
+ *   gcc -O2 -std=gnu11 -ffp-contract=off -Ioracle -o /tmp/dsteps profiles/decision_steps_drv.c oracle/cpu_ref.c -lm -lpthread
+ *   /tmp/dsteps NCH FRAMES BLOCK [EBN0] */
 #include <stdio.h>
 #include <stdlib.h>
 #include "cpu_ref.h"
-extern int g_dstep;
 int main(int argc, char** argv) {
     int nch = atoi(argv[1]), nf = atoi(argv[2]), blk = atoi(argv[3]);
     double eb = argc > 4 ? atof(argv[4]) : 1000.0;
@@ -14,7 +16,7 @@ int main(int argc, char** argv) {
         uint8_t bits[QC_BITS];
         for (int n = 0; n < nf; n++) {
             vd[c * nf + n] = qc_rx_frame(&ch, x + ((size_t)c * nf + n) * QC_FRAME, bits, NULL);
-            ds[c * nf + n] = g_dstep;
+            ds[c * nf + n] = qc_decision_step;
         }
     }
     /* per block of blk channels and frame: max decision step */
