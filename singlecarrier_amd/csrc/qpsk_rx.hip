@@ -107,6 +107,7 @@ struct RxArgs {
                              // issue priority boost (0 none, 1 front, 2 back);
                              // bits 8-15: front stagger; bits 16-19: front split
     int* err;                // device error word (kErrStall)
+    const float2* heads;     // [nch][F][102] head pre-pass outputs (HP), or null
 };
 
 // Diagnostic build only (-DQPSK_STAMPS): per-phase cycle sums of the front
@@ -411,9 +412,9 @@ __device__ __forceinline__ void fir_dec(int lane, int rt, const float2* M, float
 // from M[kM1 + 2l + s], s < 50, read as 16-B sample pairs (lane stride 16 B:
 // ds_read_b128's lane groups cover the 64 banks once; a b64 read at that
 // stride is 2-way conflicted).  It does not depend on rx_timing.
-__device__ __forceinline__ void fir_head(int lane, const float2* M, float2* dec) {
+__device__ __forceinline__ void fir_head_at(int lane, const float2* H, float2* out) {
     if (lane < 51) {
-        const float2* b = M + kM1 + 2 * lane;
+        const float2* b = H + 2 * lane;
         f2 y[2] = {{0.0f, 0.0f}, {0.0f, 0.0f}};
 #pragma unroll
         for (int s0 = 0; s0 < 50; s0 += 10) {
@@ -435,8 +436,53 @@ __device__ __forceinline__ void fir_head(int lane, const float2* M, float2* dec)
             }
         }
         const f2 o0 = y[0] * QK_GAIN, o1 = y[1] * QK_GAIN;   // one 16-B store
-        *reinterpret_cast<float4*>(dec + QK_NDEC + 2 * lane) = make_float4(o0.x, o0.y, o1.x, o1.y);
+        *reinterpret_cast<float4*>(out + 2 * lane) = make_float4(o0.x, o0.y, o1.x, o1.y);
     }
+}
+__device__ __forceinline__ void fir_head(int lane, const float2* M, float2* dec) {
+    fir_head_at(lane, M + kM1, dec + QK_NDEC);
+}
+
+// ---------------------------------------------------------------- head pre-pass
+// SURVEY.md 8f rank 4, as an execution strategy (QPSK_HEADPASS=1; not the
+// default, measured slower: profiles/r03_headpass_ab.txt).  F_{n+1}[0..101],
+// the undecimated FIR head that dec_{n+1} ends with, does not depend on
+// rx_timing, so it is computed for every frame of the call at once, ahead of
+// the serial frame loop: one wave per channel-frame mixes the 152 samples the
+// head reads -- x_{n-1}[1832..1879] ++ x_n[0..103], each (-1)^k P[t] x 2^-14
+// for its global frame k, as mix_item -- and runs the front's fir_head on
+// them.  The fronts of the frame loop then copy the 102 outputs into dec
+// instead of filtering (front_channel<.., HP>).
+constexpr int kHeadM = 152;
+constexpr int kHeadOut = QK_NHEAD;   // 102 outputs per channel-frame
+__global__ void __launch_bounds__(256) head_kernel(const int16_t* in, const int16_t* hist,
+                                                  const float2* ptab, float2* heads, int nch,
+                                                  int F, unsigned g0) {
+    __shared__ __attribute__((aligned(16))) float2 Mh[4][kHeadM];
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const size_t cf = (size_t)blockIdx.x * 4 + w;   // channel-frame ch * F + n
+    if (cf >= (size_t)nch * F) return;              // wave-uniform
+    const int ch = (int)(cf / (size_t)F), n = (int)(cf % (size_t)F);
+    const unsigned g = g0 + (unsigned)n;            // global index of frame n
+    const int16_t* xm1 = n >= 1 ? in + ((size_t)ch * F + (n - 1)) * QK_FRAME
+                                : hist + ((size_t)ch * 2 + 1) * QK_FRAME;
+    const int16_t* x0 = in + ((size_t)ch * F + n) * QK_FRAME;
+    float2* H = Mh[w];
+    for (int e = lane; e < kHeadM / 2; e += 64) {   // item e: two samples
+        const bool prev = e < 24;                   // x_{n-1} tail, else x_n head
+        const int t = prev ? 1832 + 2 * e : 2 * (e - 24);
+        const int r = *reinterpret_cast<const int*>((prev ? xm1 : x0) + t);
+        const float4 p = *reinterpret_cast<const float4*>(ptab + t);
+        const float v0 = (float)(int16_t)(r & 0xffff);
+        const float v1 = (float)(int16_t)(r >> 16);
+        const unsigned k = prev ? g - 1u : g;       // (-1)^k
+        const float sg = (k & 1u) ? -1.0f : 1.0f;   // exact sign flip
+        *reinterpret_cast<float4*>(H + 2 * e) =
+            make_float4((sg * p.x) * v0, (sg * p.y) * v0, (sg * p.z) * v1, (sg * p.w) * v1);
+    }
+    wave_lds_sync();
+    fir_head_at(lane, H, heads + cf * kHeadOut);
 }
 
 // correlate (src/qpsk.c:88-96) for all 128 lags of dec and the hunt's argmax
@@ -482,15 +528,23 @@ __device__ __forceinline__ int hunt(int lane, float2* M, const float2* dec, cons
 
 // One channel of frame n's front: D_n (decimated with rx_timing rt), F_{n+1},
 // correlation of dec_{n+1} = [D_n, F_{n+1}] and its argmax mi.
-template <int MODE>
+// HP (QPSK_HEADPASS): F_{n+1} comes from the head pre-pass (head_kernel), at
+// `head` (global, 51 x 16 B), instead of the head FIR.
+template <int MODE, bool HP = false>
 __device__ __forceinline__ int front_channel(int lane, int rt, float2* M, float2* dec,
-                                             const float* BT FACC_PARAM) {
+                                             const float* BT, const float2* head FACC_PARAM) {
 #ifdef QPSK_STAMPS
     unsigned long long ft0 = stamp_now();
 #endif
     if constexpr ((MODE & 1) != 0) {
         fir_dec752(lane, rt, M, dec);
         FSTAMP(0);
+    } else if constexpr (HP) {
+        float4 h = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (lane < kHeadOut / 2) h = reinterpret_cast<const float4*>(head)[lane];   // under the FIR
+        fir_dec(lane, rt, M, dec);
+        FSTAMP(0);
+        if (lane < kHeadOut / 2) *reinterpret_cast<float4*>(dec + QK_NDEC + 2 * lane) = h;
     } else {
         fir_dec(lane, rt, M, dec);
         FSTAMP(0);
@@ -1244,7 +1298,9 @@ __global__ void __launch_bounds__(256) rx_data_kernel(const float4* jobs, unsign
 template <int G, int FP, int MODE, bool DUAL, int W, bool QUAD>
 constexpr int kBackWavesOf = DUAL ? 2 * G * (QUAD ? W / 16 : 1) : G;
 
-template <int G, int FP, int MODE, bool DUAL, int W = QK_GROUP, bool QUAD = false>
+//
+// HP: the fronts take F_{n+1} from the head pre-pass (head_kernel, QPSK_HEADPASS).
+template <int G, int FP, int MODE, bool DUAL, int W = QK_GROUP, bool QUAD = false, bool HP = false>
 __global__ void __launch_bounds__(64 * (kBackWavesOf<G, FP, MODE, DUAL, W, QUAD> + G * FP), 3) rx_kernel(
     const int16_t* in, int16_t* hist, const float2* ptab, const unsigned long long* ks,
     float2* win0, float2* win1, int* mi0, int* mi1, int* rt0, int* rt1, uint8_t* bits,
@@ -1259,7 +1315,9 @@ __global__ void __launch_bounds__(64 * (kBackWavesOf<G, FP, MODE, DUAL, W, QUAD>
     constexpr int kFrontWaves = kGroups * kFrontPer;
     constexpr int kBlock = 64 * (kBackWaves + kFrontWaves);
     const RxArgs a{in, hist, ptab, ks, win0, win1, mi0, mi1, rt0, rt1, bits, valid, trace, soft,
-                   jobs, njobs, nch, F, g0, (size_t)jcap, roles, err};
+                   jobs, njobs, nch, F, g0, (size_t)jcap, roles, err,
+                   // HP (reference mode only): fft_tab carries the head pre-pass outputs
+                   HP ? reinterpret_cast<const float2*>(fft_tab) : nullptr};
     __shared__ __attribute__((aligned(16))) float2 P[QK_FRAME];
     constexpr int DM = MODE & 1;   // decimation semantics; MODE & 2: FFT hunt
     constexpr int kM = Cfg<DM>::kM, kDecBuf = Cfg<DM>::kDecBuf;
@@ -1412,7 +1470,8 @@ __global__ void __launch_bounds__(64 * (kBackWavesOf<G, FP, MODE, DUAL, W, QUAD>
                         }
                         wave_lds_sync();
                         STAMP(1);
-                        pmi = front_channel<MODE>(lane, rt_s[gi][p][i0 + c], M, dcur, BT FACC_ARG);
+                        pmi = front_channel<MODE, HP>(lane, rt_s[gi][p][i0 + c], M, dcur, BT,
+                                                      a.heads + ((size_t)ch * a.F + n) * kHeadOut FACC_ARG);
                         if (lane == 0) mi_s[gi][p ^ 1][i0 + c] = pmi;
                         if (c + 1 == nl) store_window(lane, pmi, dcur, wout + (size_t)ch * kWinStride);
                         wave_lds_sync();
@@ -1507,7 +1566,8 @@ __global__ void __launch_bounds__(64 * (kBackWavesOf<G, FP, MODE, DUAL, W, QUAD>
                 }
                 wave_lds_sync();
                 STAMP(1);
-                pmi = front_channel<MODE>(lane, rt_s[gi][p][cbeg + c], M, dcur, BT FACC_ARG);
+                pmi = front_channel<MODE, HP>(lane, rt_s[gi][p][cbeg + c], M, dcur, BT,
+                                              a.heads + ((size_t)ch * a.F + n) * kHeadOut FACC_ARG);
                 if (lane == 0) mi_s[gi][p ^ 1][cbeg + c] = pmi;
                 if (c + 1 == nlive) store_window(lane, pmi, dcur, wout + (size_t)ch * kWinStride);
                 wave_lds_sync();
@@ -1583,6 +1643,9 @@ struct qpsk_ctx {
     int width = 0;              // dual-chain group width forced by QPSK_WIDTH; 0: by batch size
     int quad = -1;              // quad-per-channel backs forced on/off by QPSK_QUAD; -1: by width
     int prio = -1;              // issue priority forced by QPSK_PRIO (0 none, 1 front, 2 back)
+    bool headpass = false;      // QPSK_HEADPASS: the FIR-head pre-pass (reference mode only)
+    float2* d_heads = nullptr;  // its outputs, [nch][F][102] for the largest call
+    size_t heads_cap = 0;       // channel-frames d_heads holds
     int* d_err = nullptr;       // [0] device error word (kErrStall), taken by qpsk_rx_sync;
                                 // [1] the value it took
     hipEvent_t done = nullptr;  // recorded after the latest call's kernels, on its stream
@@ -1679,6 +1742,7 @@ static void ctx_free(qpsk_ctx* c) {
     (void)hipFree(c->d_ks);
     (void)hipFree(c->d_hist);
     (void)hipFree(c->d_fft);
+    (void)hipFree(c->d_heads);
     for (int p = 0; p < 2; p++) {
         (void)hipFree(c->d_win[p]);
         (void)hipFree(c->d_mi[p]);
@@ -1754,6 +1818,7 @@ extern "C" qpsk_ctx* qpsk_rx_create_mode(int device, int nch, int mode, int* err
         c->width = (v == 16 || v == 32 || v == 64) ? v : 0;
     }
     if (const char* qv = getenv("QPSK_QUAD")) c->quad = atoi(qv) != 0;
+    if (const char* hv = getenv("QPSK_HEADPASS")) c->headpass = atoi(hv) != 0 && mode == QPSK_MODE_REFERENCE;
     if (const char* pv = getenv("QPSK_PRIO"))
         c->prio = !strcmp(pv, "none") ? 0 : !strcmp(pv, "front") ? 1 : !strcmp(pv, "back") ? 2 : -1;
     if (const char* sh = getenv("QPSK_SHAPE")) {
@@ -1858,6 +1923,15 @@ int qpsk_rx_launch(qpsk_ctx* c, const int16_t* d_in, int F, uint8_t* d_bits, uin
         HCHECK(hipMalloc(&c->d_jobs, sizeof(float4) * kJobF4 * need));
         c->jobs_cap = need;
     }
+    const bool hp = c->headpass;
+    if (hp && need > c->heads_cap) {
+        HCHECK(hipDeviceSynchronize());   // an earlier call may still read the heads
+        (void)hipFree(c->d_heads);
+        c->d_heads = nullptr;
+        c->heads_cap = 0;
+        HCHECK(hipMalloc(&c->d_heads, sizeof(float2) * kHeadOut * need));
+        c->heads_cap = need;
+    }
     int slot = -1;
     if (c->timing) {
         if (c->ev_n == qpsk_ctx::kEv) {   // pool full: fold pending spans into the totals
@@ -1877,28 +1951,38 @@ int qpsk_rx_launch(qpsk_ctx* c, const int16_t* d_in, int F, uint8_t* d_bits, uin
     }
     const int parity = (int)(c->calls & 1u);
     const Shape sh = pick_shape(c);
-#define QPSK_LAUNCH(GG, FF, MM, DD, WW, QQ)                                                    \
-    hipLaunchKernelGGL((rx_kernel<GG, FF, MM, DD, WW, QQ>),                                    \
+#define QPSK_LAUNCH(GG, FF, MM, DD, WW, QQ, HH)                                                \
+    hipLaunchKernelGGL((rx_kernel<GG, FF, MM, DD, WW, QQ, HH>),                                \
                        dim3((unsigned)((c->nch + (size_t)GG * WW - 1) / ((size_t)GG * WW))),   \
                        dim3(64 * (kBackWavesOf<GG, FF, MM, DD, WW, QQ> + GG * FF)), 0, s,      \
                        d_in, c->d_hist, c->d_ptab,                                             \
                        c->d_ks, c->d_win[0], c->d_win[1], c->d_mi[0], c->d_mi[1], c->d_rt[0],  \
                        c->d_rt[1], d_bits, d_valid, d_trace, reinterpret_cast<float2*>(d_soft), \
                        c->d_jobs, c->d_njobs + parity, c->nch, F,                               \
-                       (unsigned)(c->frames & 0xffffffffu), sh.roles, c->d_fft,                \
+                       (unsigned)(c->frames & 0xffffffffu), sh.roles,                          \
+                       HH ? reinterpret_cast<const float*>(c->d_heads) : c->d_fft,             \
                        (unsigned long long)c->jobs_cap, d_err)
-#define QPSK_LAUNCH_MODE(MM)                                                                   \
+#define QPSK_LAUNCH_SHAPES(MM, HH)                                                             \
     do {                                                                                       \
         switch (sh.kind) {                                                                     \
-            case Shape::k2x4d: QPSK_LAUNCH(2, 4, MM, true, 64, false); break;              \
-            case Shape::k1x8d16: QPSK_LAUNCH(1, 8, MM, true, 16, false); break;            \
-            case Shape::k1x8d32: QPSK_LAUNCH(1, 8, MM, true, 32, false); break;            \
-            case Shape::k1x8d64: QPSK_LAUNCH(1, 8, MM, true, 64, false); break;            \
-            case Shape::k1x8q16: QPSK_LAUNCH(1, 8, MM, true, 16, true); break;             \
-            case Shape::k1x8q32: QPSK_LAUNCH(1, 8, MM, true, 32, true); break;             \
-            default: QPSK_LAUNCH(4, 2, MM, false, 64, false); break;                           \
+            case Shape::k2x4d: QPSK_LAUNCH(2, 4, MM, true, 64, false, HH); break;              \
+            case Shape::k1x8d16: QPSK_LAUNCH(1, 8, MM, true, 16, false, HH); break;            \
+            case Shape::k1x8d32: QPSK_LAUNCH(1, 8, MM, true, 32, false, HH); break;            \
+            case Shape::k1x8d64: QPSK_LAUNCH(1, 8, MM, true, 64, false, HH); break;            \
+            case Shape::k1x8q16: QPSK_LAUNCH(1, 8, MM, true, 16, true, HH); break;             \
+            case Shape::k1x8q32: QPSK_LAUNCH(1, 8, MM, true, 32, true, HH); break;             \
+            default: QPSK_LAUNCH(4, 2, MM, false, 64, false, HH); break;                       \
         }                                                                                      \
     } while (0)
+#define QPSK_LAUNCH_MODE(MM) QPSK_LAUNCH_SHAPES(MM, false)
+    if (hp) {   // head pre-pass: every channel-frame's F_{n+1}, then the frame loop
+        const size_t ncf = (size_t)c->nch * (size_t)F;
+        hipLaunchKernelGGL(head_kernel, dim3((unsigned)((ncf + 3) / 4)), dim3(256), 0, s, d_in,
+                           c->d_hist, c->d_ptab, c->d_heads, c->nch, F,
+                           (unsigned)(c->frames & 0xffffffffu));
+        HCHECK(hipGetLastError());
+        QPSK_LAUNCH_SHAPES(0, true);
+    } else
     switch (c->mode) {
         case 0: QPSK_LAUNCH_MODE(0); break;
         case 1: QPSK_LAUNCH_MODE(1); break;
@@ -1906,6 +1990,7 @@ int qpsk_rx_launch(qpsk_ctx* c, const int16_t* d_in, int F, uint8_t* d_bits, uin
         default: QPSK_LAUNCH_MODE(3); break;
     }
 #undef QPSK_LAUNCH_MODE
+#undef QPSK_LAUNCH_SHAPES
 #undef QPSK_LAUNCH
     HCHECK(hipGetLastError());
     if (slot >= 0) HCHECK(hipEventRecord(c->ev[slot][1], s));

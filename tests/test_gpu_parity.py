@@ -263,6 +263,50 @@ def test_dual_chain_group_widths(width, quad, monkeypatch):
     _vs_oracle(x)
 
 
+@pytest.mark.parametrize("shape,width,quad", [("4x2", None, None), ("2x4d", None, None),
+                                               ("1x8", "64", "0"), ("1x8", "32", "1"),
+                                               ("1x8", "16", "1")])
+def test_head_prepass(shape, width, quad, monkeypatch):
+    """SURVEY.md 8f rank 4, the frame-parallel FIR-head pre-pass
+    (QPSK_HEADPASS=1): head_kernel computes every channel-frame's
+    rx_timing-independent F_{n+1}[0..101] ahead of the frame loop and the
+    fronts copy it instead of filtering.  Every shape, a ragged AWGN batch
+    with silent and saturated channels, every output exact."""
+    monkeypatch.setenv("QPSK_HEADPASS", "1")
+    monkeypatch.setenv("QPSK_SHAPE", shape)
+    if width:
+        monkeypatch.setenv("QPSK_WIDTH", width)
+        monkeypatch.setenv("QPSK_QUAD", quad)
+    x = oracle.synth(95, 300, 11, 5.0)
+    x[7] = 0
+    x[8] = 32767
+    _vs_oracle(x)
+
+
+def test_head_prepass_across_call_splits(monkeypatch):
+    """The pre-pass reads frame n-1's tail from the carried history for a
+    call's first frame: calls of 1, 1, 4, 1 and the remaining frames."""
+    monkeypatch.setenv("QPSK_HEADPASS", "1")
+    nch, nf = 260, 12
+    x = oracle.synth(96, nch, nf, 4.0)
+    bits, valid, tr = oracle.cpu_rx(x, trace=True)
+    rx = sc.Receiver(nch)
+    parts, a = [], 0
+    for b in (1, 2, 6, 7, nf):
+        parts.append(rx.demod(np.ascontiguousarray(x[:, a:b]), trace=True, soft=True))
+        a = b
+    out = {k: np.concatenate([p[k] for p in parts], axis=1) for k in ("bits", "valid", "trace", "soft")}
+    _assert_same(out, bits, valid, tr)
+
+
+@pytest.mark.parametrize("nch", [8192, 16384])
+def test_head_prepass_c4_shards(nch, monkeypatch):
+    """The pre-pass at the C4 N = 8 and N = 4 shard sizes (x 32 frames, AWGN)."""
+    monkeypatch.setenv("QPSK_HEADPASS", "1")
+    x = oracle.synth(97, nch, 32, 6.0)
+    _vs_oracle(x)
+
+
 @pytest.mark.parametrize("ebn0", [1000.0, 6.0, 0.0])
 def test_quad_back_edges_and_noise(ebn0, monkeypatch):
     """The quad-per-channel back on saturated, zero and constant channels next
@@ -299,6 +343,7 @@ def test_c4_shards_at_size(ngpu, c0):
     nch = 65536 // ngpu
     x = oracle.synth(81, nch, 32, 6.0, c0=c0)
     _vs_oracle(x)
+
 
 
 def test_progress_wait_timeout_is_an_error(monkeypatch):
