@@ -32,7 +32,7 @@ ncu = torch.cuda.get_device_properties(0).multi_processor_count
 W = int(os.environ.get("QPSK_WIDTH", "0")) or (16 if nch <= 16 * ncu else 32 if nch <= 32 * ncu else 64)
 quad = int(os.environ.get("QPSK_QUAD", "1" if W <= 32 else "0"))
 nwg = (nch + W - 1) // W
-back_waves = nwg * 2 * (W // 16 if quad else 1)
+back_waves = nwg * 2 * (W // (16 * quad) if quad else 1)
 front_waves = nwg * 8
 x = torch.from_numpy(sc.synth(3, nch, nf)).cuda()
 bits = torch.empty((nch, nf, 62), dtype=torch.uint8, device="cuda")
