@@ -1,0 +1,18 @@
+#!/bin/bash
+# Pair backs (QPSK_QUAD=2) under each issue priority (QPSK_PRIO: the back or
+# the front waves raised with s_setprio, or none) against the default shape,
+# interleaved, R rounds.  Each line: label, channels, ms per step, kernel us, verified.
+R=${1:-2}
+run() { # label nch [env...]
+  local label=$1 nch=$2; shift 2
+  env "$@" timeout -k 10 300 python bench.py --channels $nch --cpu-channels 0 \
+    --cpu-all-channels 0 --stream-chunks 0 --verify 64 --steps 5 --warmup 2 \
+    | python -c "import sys,json; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); print('$label', $nch, d['ms_per_step'], d['roofline']['kernels_us'], d['verified_vs_oracle'])"
+}
+for r in $(seq 1 $R); do
+  run lane 16384 || exit 1
+  run pair-prio-back 16384 QPSK_QUAD=2 QPSK_PRIO=back || exit 1
+  run pair-prio-none 16384 QPSK_QUAD=2 QPSK_PRIO=none || exit 1
+  run quad 8192 || exit 1
+  run pair-prio-back 8192 QPSK_QUAD=2 QPSK_PRIO=back || exit 1
+done
