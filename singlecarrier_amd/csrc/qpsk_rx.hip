@@ -1170,273 +1170,6 @@ __device__ __forceinline__ void back_frame_quad(const RxArgs& a, int ch, bool li
     }
 }
 
-// ---------------------------------------------------------------- pair back
-// The 16,384-channel shard (dual chain, W = 64) waits for its front batch
-// because one lane-per-channel back wave holds a whole group; quads need 16
-// waves there.  A PAIR of lanes per channel puts 32 channels in a wave, so a
-// group of 64 splits into two channel blocks per chain within 12 waves.  Lane
-// c (0, 1) of a pair does the work of quad lanes c and 3 - c:
-//   columns jA = 1 + c and jB = 4 - c (f, g, s, y, d, h; 5 terms of f each)
-//   rows rA = c and rB = 3 - c, each row's chain of 6.15/6.16 updates:
-//     RA[k] = u[c][k+1]  (k = 0..3; lane 1's RA[0] is padding)
-//     RB[k] = u[3-c][k+3] (k = 0..1; lane 0's RB[0] is padding)
-//   eq[c], eq[3-c], eq[4] (lane 0), d[0], d[jA], d[jB].
-// Column j's h and g reach both lanes by DPP broadcast; the prefix sums a[j]
-// and val run in column / tap order over the pair.  Every fp32 operation is
-// one update_eq() issues, on the same operands, in the same order; padding
-// (zero u entries, zero-masked h) enters only as +-0 addends or factors of
-// finite values, as in the quad layout.
-namespace pd {
-constexpr int kP0 = 0xA0;   // quad_perm [0,0,2,2]: broadcast lane 0 of the pair
-constexpr int kP1 = 0xF5;   // [1,1,3,3]: broadcast lane 1 of the pair
-constexpr int kSw = 0xB1;   // [1,0,3,2]: the other lane of the pair
-}
-
-struct PKal {
-    f2 RA[4], RB[2];
-    f2 eqA, eqB, eq4;
-    float d0, dA, dB;
-};
-
-__device__ __forceinline__ PKal pkal_reset() {   // kalman_reset, src/kalman.c:42-55
-    PKal k;
-#pragma unroll
-    for (int i = 0; i < 4; i++) k.RA[i] = f2{0.0f, 0.0f};
-    k.RB[0] = k.RB[1] = f2{0.0f, 0.0f};
-    k.eqA = k.eqB = k.eq4 = f2{0.0f, 0.0f};
-    k.d0 = k.dA = k.dB = 1.0f;
-    return k;
-}
-
-// one row's chain of 6.15/6.16 updates at one column: h, g of the column
-__device__ __forceinline__ void prow(f2& u, f2& G, f2 h, f2 gcol) {
-    const f2 B1 = u;
-    u = B1 + cmulc(h, G);
-    G = G + cmulc(gcol, B1);
-}
-
-// one train_eq step (update_eq<EXACT>'s operations) on the pair layout.
-// XA[d] = x[c-1+d] (d < 3), XB[d] = x[d-c] (d < 5): x[index+t] of the
-// reference, zero before x[0].  Returns er = Re(error).
-template <bool EXACT>
-__device__ __forceinline__ float pstep(PKal& k, const f2 (&XA)[3], const f2 (&XB)[5], float ref,
-                                       int c, bool& bad) {
-    const float E = QK_KAL_E, q = QK_KAL_Q;
-    const float m1 = c == 0 ? 1.0f : 0.0f;   // lane 0
-    const float m0 = 1.0f - m1;              // lane 1 (exactly 0 or 1)
-    // val = sum_t x[t] * eq[t], t = 0..4 in order: t = 0, 3, 4 on lane 0, 1, 2 on lane 1
-    const f2 pA = cmul(XA[1], k.eqA);        // x[c] * eq[c]
-    const f2 pB = cmul(XB[3], k.eqB);        // x[3-c] * eq[3-c]
-    const f2 p4 = cmul(XB[4], k.eq4);        // lane 0: x[4] * eq[4]
-    float vr = 0.0f, vi = 0.0f;
-#define PV(CT, P)                                                   \
-    vr = vr + qdf<CT>(P.x); vi = vi + qdf<CT>(P.y);                 \
-    asm("" : "+v"(vr), "+v"(vi))
-    PV(pd::kP0, pA); PV(pd::kP1, pA); PV(pd::kP1, pB); PV(pd::kP0, pB); PV(pd::kP0, p4);
-#undef PV
-    const float er = ref - vr;               // conjf(ref - val) = (ref - vr, vi)
-    // column 0: f0 = conj(x0), 6.2
-    const f2 x0 = qd2<pd::kP0>(XA[1]);
-    const f2 f0 = conj2(x0);
-    const f2 g0 = f0 * k.d0;                 // 6.4
-    const f2 t0 = g0 * f0;
-    const float a0 = E + (t0.x + t0.y);      // 6.5
-    // this step's column terms from the rows (pads: zero u entries)
-    const f2 cA0 = qd2<pd::kP0>(k.RA[1]) * m0;                 // lane 1: u02; lane 0: pad
-    const f2 cA1 = c ? k.RA[1] : k.RA[0];                      // u12 / u01
-    const f2 cB0 = k.RA[3] * m1;                               // lane 0: u04; lane 1: pad
-    const f2 cB1 = qd2<pd::kSw>(c ? k.RA[3] : k.RA[2]);        // u03 / u14
-    const f2 wB2 = qd2<pd::kSw>(k.RB[1]);
-    const f2 cB2 = c ? k.RA[2] : wB2;                          // u13 / u24
-    const f2 cB3 = c ? k.RB[0] : k.RB[1];                      // u23 / u34
-    // column jA: f = u[jA-2][jA]*conj(x[jA-2]) + conj(x[jA]) + u[jA-1][jA]*conj(x[jA-1])
-    f2 fA = addc(cmulc(cA0, XA[0]), XA[2]);
-    fA = fA + cmulc(cA1, XA[1]);
-    f2 fB = addc(cmulc(cB0, XB[0]), XB[4]);
-    fB = fB + cmulc(cB1, XB[1]);
-    fB = fB + cmulc(cB2, XB[2]);
-    fB = fB + cmulc(cB3, XB[3]);
-    const f2 gA = fA * k.dA, gB = fB * k.dB;                   // 6.4
-    const f2 tA = gA * fA, tB = gB * fB;
-    const float sA = tA.x + tA.y, sB = tB.x + tB.y;
-    // 6.6 a[j] = a[j-1] + Re(g conj f) in column order: 1 (lane 0 A), 2 (lane 1 A),
-    // 3 (lane 1 B), 4 (lane 0 B)
-    const float a1 = a0 + qdf<pd::kP0>(sA);
-    const float a2 = a1 + qdf<pd::kP1>(sA);
-    const float a3 = a2 + qdf<pd::kP1>(sB);
-    const float a4 = a3 + qdf<pd::kP0>(sB);
-    const float hq = 1.0f + q;                                 // 6.7
-    const float ht = a4 * q;
-    const float apA = c ? a1 : a0, aoA = c ? a2 : a1;          // a[jA-1], a[jA]
-    const float apB = c ? a2 : a3, aoB = c ? a3 : a4;          // a[jB-1], a[jB]
-    const float xs0 = a0 + ht, xsA = aoA + ht, xsB = aoB + ht;
-    float y0, yA, yB;
-    if (EXACT) {
-        y0 = qk_div_ieee(xs0);
-        yA = qk_div_ieee(xsA);
-        yB = qk_div_ieee(xsB);
-    } else {
-        bad |= !qk_rcp_in_range(xs0, xsB);   // xs is nondecreasing in j (update_eq)
-        y0 = qk_rcp_fast(xs0);
-        yA = qk_rcp_fast(xsA);
-        yB = qk_rcp_fast(xsB);
-    }
-    k.d0 = k.d0 * ((hq * (E + ht)) * y0);                      // 6.20
-    k.dA = k.dA * ((hq * (apA + ht)) * yA);                    // 6.21, 6.13
-    k.dB = k.dB * ((hq * (apB + ht)) * yB);
-    // h[j] = -f[j] * y[j-1] (6.11): y[jA-1] = y0 / y1 (lane 0's yA), y[jB-1] =
-    // y3 (lane 1's yB) / y2 (lane 1's yA)
-    const float y1 = qdf<pd::kP0>(yA), y3 = qdf<pd::kP1>(yB);
-    const f2 hA = (-fA) * (c ? y1 : y0);
-    const f2 hB = (-fB) * (c ? yA : y3);
-    // every column's h and (original) g on both lanes
-    const f2 H1 = qd2<pd::kP0>(hA), G1 = qd2<pd::kP0>(gA);
-    const f2 H2 = qd2<pd::kP1>(hA), G2 = qd2<pd::kP1>(gA);
-    const f2 H3 = qd2<pd::kP1>(hB), G3 = qd2<pd::kP1>(gB);
-    const f2 H4 = qd2<pd::kP0>(hB), G4 = qd2<pd::kP0>(gB);
-    // row c: columns 1 (lane 1: padding), 2, 3, 4, from g[c]
-    f2 GA = c ? G1 : g0;
-    prow(k.RA[0], GA, H1 * m1, G1);
-    prow(k.RA[1], GA, H2, G2);
-    prow(k.RA[2], GA, H3, G3);
-    prow(k.RA[3], GA, H4, G4);
-    // row 3-c: columns 3 (lane 0: padding), 4, from g[3-c]
-    f2 GB = c ? G2 : G3;
-    prow(k.RB[0], GB, H3 * m0, G3);
-    prow(k.RB[1], GB, H4, G4);
-    // update_eq: error *= kalman_y (y[4], lane 0's yB); eq[i] += error * conj(g[i])
-    const float y4 = qdf<pd::kP0>(yB);
-    const f2 e = f2{er, vi} * y4;
-    k.eqA = k.eqA + cmulc(e, GA);
-    k.eqB = k.eqB + cmulc(e, GB);
-    k.eq4 = k.eq4 + cmulc(e, G4);            // lane 0: g[4] (row 4 has no updates)
-    return er;
-}
-
-// step 0: XA[d] = x[c-1+d], XB[d] = x[d-c]; window slot k+1 = x[k] = dec[mi+k]
-__device__ __forceinline__ void pload_x0(const f2* wp2, int c, f2 (&XA)[3], f2 (&XB)[5]) {
-#pragma unroll
-    for (int d = 0; d < 3; d++) XA[d] = c - 1 + d >= 0 ? wp2[c + d] : f2{0.0f, 0.0f};
-#pragma unroll
-    for (int d = 0; d < 5; d++) XB[d] = d - c >= 0 ? wp2[d - c + 1] : f2{0.0f, 0.0f};
-}
-
-// 128 steps; the two window streams (XA[2] = x[s+c+1] = wa[s], XB[4] =
-// x[s+4-c] = wb[s]) arrive through 4-step rings loaded an iteration ahead, as
-// qtrain's.  The reads run to slot 134, inside the 168-slot row.
-template <bool EXACT>
-__device__ __forceinline__ int ptrain(PKal& k, f2 (&XA)[3], f2 (&XB)[5], const f2* wa, const f2* wb,
-                                      int c, bool& bad) {
-    int matches = 0;
-    f2 BA[4], BB[4];
-#pragma unroll
-    for (int t = 0; t < 4; t++) {
-        BA[t] = wa[t + 1];
-        BB[t] = wb[t + 1];
-    }
-    for (int i = 0; i < QK_NPRE; i += 4) {
-        f2 NA[4], NB[4];
-#pragma unroll
-        for (int t = 0; t < 4; t++) {
-            NA[t] = wa[i + 5 + t];
-            NB[t] = wb[i + 5 + t];
-        }
-#pragma unroll
-        for (int t = 0; t < 4; t++) {
-            const int st = i + t;
-            const unsigned long long m = st < 64 ? kPreLo : kPreHi;
-            const float ref = ((m >> (st & 63)) & 1ull) ? 1.0f : -1.0f;
-            const float er = pstep<EXACT>(k, XA, XB, ref, c, bad);
-            if (er * ref > 0.0f) matches++;
-            XA[0] = XA[1];
-            XA[1] = XA[2];
-            XA[2] = BA[t];
-#pragma unroll
-            for (int d = 0; d < 4; d++) XB[d] = XB[d + 1];
-            XB[4] = BB[t];
-        }
-#pragma unroll
-        for (int t = 0; t < 4; t++) {
-            BA[t] = NA[t];
-            BB[t] = NB[t];
-        }
-    }
-    return matches;
-}
-
-// back_frame() for a pair of lanes per channel: both lanes of a pair have the
-// same matches / valid / rt; the pair's lane 0 writes the per-channel outputs.
-template <typename RtFn>
-__device__ __forceinline__ void back_frame_pair(const RxArgs& a, int ch, bool live, int n, int mi,
-                                                RtFn get_rt, const float2* win, int* rt_next) {
-    const int c = lane_id() & 1;
-    const bool lead = c == 0;
-    const f2* wp2 = reinterpret_cast<const f2*>(win);
-    PKal k = pkal_reset();
-    f2 XA[3], XB[5];
-    pload_x0(wp2, c, XA, XB);
-    bool bad = (a.roles & kForceExact) != 0;
-    int matches = ptrain<false>(k, XA, XB, wp2 + c + 2, wp2 + 5 - c, c, bad);
-    if (__builtin_expect(__ballot(bad) != 0ull, 0)) {   // recompute the frame exactly
-        k = pkal_reset();
-        pload_x0(wp2, c, XA, XB);
-        matches = ptrain<true>(k, XA, XB, wp2 + c + 2, wp2 + 5 - c, c, bad);
-    }
-    const bool valid = live && matches > QK_MATCH_MIN;   // src/qpsk.c:196
-    const size_t cf = (size_t)ch * a.F + n;
-    const unsigned long long vm = __ballot(valid && lead);
-    if (vm) {   // gather the pair's state (both lanes take part in the DPP moves)
-        DataJob j;
-        j.k.eq[0] = qd2<pd::kP0>(k.eqA);
-        j.k.eq[1] = qd2<pd::kP1>(k.eqA);
-        j.k.eq[2] = qd2<pd::kP1>(k.eqB);
-        j.k.eq[3] = qd2<pd::kP0>(k.eqB);
-        j.k.eq[4] = qd2<pd::kP0>(k.eq4);
-        j.k.u[uix(0, 1)] = qd2<pd::kP0>(k.RA[0]);
-        j.k.u[uix(0, 2)] = qd2<pd::kP0>(k.RA[1]);
-        j.k.u[uix(0, 3)] = qd2<pd::kP0>(k.RA[2]);
-        j.k.u[uix(0, 4)] = qd2<pd::kP0>(k.RA[3]);
-        j.k.u[uix(1, 2)] = qd2<pd::kP1>(k.RA[1]);
-        j.k.u[uix(1, 3)] = qd2<pd::kP1>(k.RA[2]);
-        j.k.u[uix(1, 4)] = qd2<pd::kP1>(k.RA[3]);
-        j.k.u[uix(2, 3)] = qd2<pd::kP1>(k.RB[0]);
-        j.k.u[uix(2, 4)] = qd2<pd::kP1>(k.RB[1]);
-        j.k.u[uix(3, 4)] = qd2<pd::kP0>(k.RB[1]);
-        const float d1 = qdf<pd::kP0>(k.dA), d2 = qdf<pd::kP1>(k.dA);
-        const float d3 = qdf<pd::kP1>(k.dB), d4 = qdf<pd::kP0>(k.dB);
-        j.k.d[0] = f2{k.d0, k.d0};
-        j.k.d[1] = f2{d1, d1};
-        j.k.d[2] = f2{d2, d2};
-        j.k.d[3] = f2{d3, d3};
-        j.k.d[4] = f2{d4, d4};
-        unsigned base = 0;
-        if (lane_id() == 0) base = atomicAdd(a.njobs, (unsigned)__popcll(vm));
-        base = __builtin_amdgcn_readfirstlane(base);
-        if (valid && lead) {
-            const unsigned slot = base + (unsigned)__popcll(vm & ((1ull << lane_id()) - 1ull));
-            j.cf = cf;
-            j.ks = (a.g0 + (unsigned)n) % QK_KS_FRAMES;
-            put_job(a.jobs, a.jcap, slot, j, wp2 + 129);
-        }
-    }
-    if (live && !valid) {   // invalid frame: bits (and soft symbols) are zero
-        uint16_t* bo = reinterpret_cast<uint16_t*>(a.bits + cf * QK_NBITS);
-        for (int ss = c; ss < QK_NDSYM; ss += 2) bo[ss] = 0;
-        if (a.soft) {
-            float2* so = a.soft + cf * QK_NDSYM;
-            for (int ss = c; ss < QK_NDSYM; ss += 2) so[ss] = make_float2(0.0f, 0.0f);
-        }
-    }
-    const int rt = get_rt();
-    const int rtn = valid ? mi + QK_NPRE : rt;    // src/qpsk.c:219
-    if (lead) *rt_next = rtn;
-    if (live && lead) {
-        a.valid[cf] = valid ? 1 : 0;
-        if (a.trace)
-            *reinterpret_cast<int4*>(a.trace + cf * 4) = make_int4(mi, matches, valid ? 1 : 0, rtn);
-    }
-}
-
 // 31 x data_eq + qpsk_demod (src/equalizer.c:64-90, src/qpsk.c:268-271) from
 // the job's window samples xs; returns the raw dibits (bit 2s = Q, 2s+1 = I).
 // Decisions collect in a register; the caller stores the 62 bytes after the
@@ -1560,27 +1293,24 @@ __global__ void __launch_bounds__(256) rx_data_kernel(const float4* jobs, unsign
 // back lanes idle but spreads a small batch over more CUs and gives each front
 // wave fewer channels per frame, which shortens the front half of the chain.
 //
-// QUAD (DUAL, G == 1 only): the back layout.  0: a lane per channel; 1: a
-// quad of lanes per channel (back_frame_quad), 16 channels per wave, W / 16
-// waves per frame chain; 2: a pair of lanes per channel (back_frame_pair), 32
-// channels per wave, W / 32 waves per frame chain.
-constexpr int kBackCh(int quad) { return quad == 1 ? 16 : quad == 2 ? 32 : 64; }
-template <int G, int FP, int MODE, bool DUAL, int W, int QUAD>
-constexpr int kBackWavesOf = DUAL ? 2 * G * (QUAD ? W / kBackCh(QUAD) : 1) : G;
+// QUAD (DUAL, G == 1 only): the back waves hold a quad of lanes per channel
+// (back_frame_quad), 16 channels per wave, W / 16 waves per frame chain.
+template <int G, int FP, int MODE, bool DUAL, int W, bool QUAD>
+constexpr int kBackWavesOf = DUAL ? 2 * G * (QUAD ? W / 16 : 1) : G;
 
 //
 // HP: the fronts take F_{n+1} from the head pre-pass (head_kernel, QPSK_HEADPASS).
-template <int G, int FP, int MODE, bool DUAL, int W = QK_GROUP, int QUAD = 0, bool HP = false>
+template <int G, int FP, int MODE, bool DUAL, int W = QK_GROUP, bool QUAD = false, bool HP = false>
 __global__ void __launch_bounds__(64 * (kBackWavesOf<G, FP, MODE, DUAL, W, QUAD> + G * FP), 3) rx_kernel(
     const int16_t* in, int16_t* hist, const float2* ptab, const unsigned long long* ks,
     float2* win0, float2* win1, int* mi0, int* mi1, int* rt0, int* rt1, uint8_t* bits,
     uint8_t* valid, int32_t* trace, float2* soft, float4* jobs, unsigned* njobs, int nch, int F,
     unsigned g0, int roles, const float* fft_tab, unsigned long long jcap, int* err) {
     static_assert(W == QK_GROUP || (DUAL && G == 1 && W % FP == 0 && W <= QK_GROUP), "group width");
-    static_assert(!QUAD || (DUAL && G == 1 && W % kBackCh(QUAD) == 0), "quad/pair backs: dual chain, one group");
+    static_assert(!QUAD || (DUAL && G == 1 && W % 16 == 0), "quad backs: dual chain, one group");
     constexpr int kGroups = G, kFrontPer = FP;
     constexpr int kBackWaves = kBackWavesOf<G, FP, MODE, DUAL, W, QUAD>;
-    constexpr int kChainWaves = QUAD ? W / kBackCh(QUAD) : 1;   // back waves per frame chain and group
+    constexpr int kChainWaves = QUAD ? W / 16 : 1;     // back waves per frame chain and group
     constexpr int kFrontCh = W / kFrontPer;            // channels per front wave
     constexpr int kFrontWaves = kGroups * kFrontPer;
     constexpr int kBlock = 64 * (kBackWaves + kFrontWaves);
@@ -1646,10 +1376,10 @@ __global__ void __launch_bounds__(64 * (kBackWavesOf<G, FP, MODE, DUAL, W, QUAD>
             // gi = (wave >> 1) / kChainWaves, block b, frames n = wave mod 2
             const int gi = (wave >> 1) / kChainWaves;
             const int b = (wave >> 1) % kChainWaves;
-            // channel of this lane within the block: the lane, its quad or its
-            // pair.  Lanes past the block (lane backs with W < 64) own no
-            // channel: they read their block's first channel's slots and write none.
-            const int sub = QUAD == 1 ? lane >> 2 : QUAD == 2 ? lane >> 1 : lane;
+            // channel of this lane within the block: the lane, or its quad.
+            // Lanes past the block (lane backs with W < 64) own no channel:
+            // they read their block's first channel's slots and write none.
+            const int sub = QUAD ? lane >> 2 : lane;
             const bool own = sub < kBlkCh;
             const int idx = kBlkCh * b + (own ? sub : 0);
             const int ch = (grp0 + gi) * W + idx;
@@ -1676,10 +1406,8 @@ __global__ void __launch_bounds__(64 * (kBackWavesOf<G, FP, MODE, DUAL, W, QUAD>
                 };
                 const float2* wn = win_of(a, a.g0 + (unsigned)n) + (size_t)(live ? ch : 0) * kWinStride;
                 int* rtn = own ? &rt_s[gi][p ^ 1][idx] : nullptr;
-                if constexpr (QUAD == 1)
+                if constexpr (QUAD)
                     back_frame_quad(a, live ? ch : 0, live, n, mi, get_rt, wn, rtn);
-                else if constexpr (QUAD == 2)
-                    back_frame_pair(a, live ? ch : 0, live, n, mi, get_rt, wn, rtn);
                 else
                     back_frame(a, live ? ch : 0, live, n, mi, get_rt, wn, rtn);
                 signal_add(&bseq[gi][p][b], 1, lane);
@@ -1760,10 +1488,10 @@ __global__ void __launch_bounds__(64 * (kBackWavesOf<G, FP, MODE, DUAL, W, QUAD>
         __syncthreads();
         if (wave < kBackWaves && (wave & 1) == 0) {   // state after the call's last frame
             const int gi = (wave >> 1) / kChainWaves;
-            const int sub = QUAD == 1 ? lane >> 2 : QUAD == 2 ? lane >> 1 : lane;
+            const int sub = QUAD ? lane >> 2 : lane;
             const int idx = kBlkCh * ((wave >> 1) % kChainWaves) + sub;
             const int ch = (grp0 + gi) * W + idx;
-            if (sub < kBlkCh && ch < a.nch && (lane & (QUAD == 1 ? 3 : QUAD == 2 ? 1 : 0)) == 0) {
+            if (sub < kBlkCh && ch < a.nch && (!QUAD || (lane & 3) == 0)) {
                 const unsigned ge = a.g0 + (unsigned)a.F;
                 mi_of(a, ge)[ch] = mi_s[gi][a.F & 1][idx];
                 rt_of(a, ge)[ch] = rt_s[gi][a.F & 1][idx];
@@ -1865,7 +1593,7 @@ float bits2f(uint32_t u) {
 
 // rx_kernel instantiations (pick_shape below)
 struct Shape {
-    enum Kind { k4x2, k2x4d, k1x8d16, k1x8d32, k1x8d64, k1x8q16, k1x8q32, k1x8p32, k1x8p64 };
+    enum Kind { k4x2, k2x4d, k1x8d16, k1x8d32, k1x8d64, k1x8q16, k1x8q32 };
     int kind;
     int roles;
 };
@@ -1913,7 +1641,7 @@ struct qpsk_ctx {
     int ncu = 256;              // compute units of the device
     int shape = -1;             // Shape::Kind forced by QPSK_SHAPE (A/B runs); -1: by batch size
     int width = 0;              // dual-chain group width forced by QPSK_WIDTH; 0: by batch size
-    int quad = -1;              // back layout forced by QPSK_QUAD (0 lane, 1 quad, 2 pair); -1: by width
+    int quad = -1;              // quad-per-channel backs forced on/off by QPSK_QUAD; -1: by width
     int prio = -1;              // issue priority forced by QPSK_PRIO (0 none, 1 front, 2 back)
     bool headpass = false;      // QPSK_HEADPASS: the FIR-head pre-pass (reference mode only)
     float2* d_heads = nullptr;  // its outputs, [nch][F][102] for the largest call
@@ -2089,7 +1817,7 @@ extern "C" qpsk_ctx* qpsk_rx_create_mode(int device, int nch, int mode, int* err
         const int v = atoi(w);
         c->width = (v == 16 || v == 32 || v == 64) ? v : 0;
     }
-    if (const char* qv = getenv("QPSK_QUAD")) c->quad = atoi(qv);   // 0 lane, 1 quad, 2 pair
+    if (const char* qv = getenv("QPSK_QUAD")) c->quad = atoi(qv) != 0;
     if (const char* hv = getenv("QPSK_HEADPASS")) c->headpass = atoi(hv) != 0 && mode == QPSK_MODE_REFERENCE;
     if (const char* pv = getenv("QPSK_PRIO"))
         c->prio = !strcmp(pv, "none") ? 0 : !strcmp(pv, "front") ? 1 : !strcmp(pv, "back") ? 2 : -1;
@@ -2160,11 +1888,8 @@ static Shape pick_shape(const qpsk_ctx* c) {
         // quad backs need W / 16 back waves per chain: at W = 64 that is 16
         // waves per workgroup, whose 128-VGPR budget spills the front; the
         // lane-per-channel back stays there (profiles/r02_quad_ab.txt)
-        // QPSK_QUAD=2: a pair of lanes per channel (W = 32 or 64)
-        const bool quad = W <= 32 && (c->quad >= 0 ? c->quad == 1 : true);
-        if (c->quad == 2 && W >= 32) {
-            sh.kind = W == 32 ? Shape::k1x8p32 : Shape::k1x8p64;
-        } else if (quad) {
+        const bool quad = W <= 32 && (c->quad >= 0 ? c->quad != 0 : true);
+        if (quad) {
             sh.kind = W == 16 ? Shape::k1x8q16 : Shape::k1x8q32;
         } else {
             sh.kind = W == 16 ? Shape::k1x8d16 : W == 32 ? Shape::k1x8d32 : Shape::k1x8d64;
@@ -2240,15 +1965,13 @@ int qpsk_rx_launch(qpsk_ctx* c, const int16_t* d_in, int F, uint8_t* d_bits, uin
 #define QPSK_LAUNCH_SHAPES(MM, HH)                                                             \
     do {                                                                                       \
         switch (sh.kind) {                                                                     \
-            case Shape::k2x4d: QPSK_LAUNCH(2, 4, MM, true, 64, 0, HH); break;                  \
-            case Shape::k1x8d16: QPSK_LAUNCH(1, 8, MM, true, 16, 0, HH); break;                \
-            case Shape::k1x8d32: QPSK_LAUNCH(1, 8, MM, true, 32, 0, HH); break;                \
-            case Shape::k1x8d64: QPSK_LAUNCH(1, 8, MM, true, 64, 0, HH); break;                \
-            case Shape::k1x8q16: QPSK_LAUNCH(1, 8, MM, true, 16, 1, HH); break;                \
-            case Shape::k1x8q32: QPSK_LAUNCH(1, 8, MM, true, 32, 1, HH); break;                \
-            case Shape::k1x8p32: QPSK_LAUNCH(1, 8, MM, true, 32, 2, HH); break;                \
-            case Shape::k1x8p64: QPSK_LAUNCH(1, 8, MM, true, 64, 2, HH); break;                \
-            default: QPSK_LAUNCH(4, 2, MM, false, 64, 0, HH); break;                           \
+            case Shape::k2x4d: QPSK_LAUNCH(2, 4, MM, true, 64, false, HH); break;              \
+            case Shape::k1x8d16: QPSK_LAUNCH(1, 8, MM, true, 16, false, HH); break;            \
+            case Shape::k1x8d32: QPSK_LAUNCH(1, 8, MM, true, 32, false, HH); break;            \
+            case Shape::k1x8d64: QPSK_LAUNCH(1, 8, MM, true, 64, false, HH); break;            \
+            case Shape::k1x8q16: QPSK_LAUNCH(1, 8, MM, true, 16, true, HH); break;             \
+            case Shape::k1x8q32: QPSK_LAUNCH(1, 8, MM, true, 32, true, HH); break;             \
+            default: QPSK_LAUNCH(4, 2, MM, false, 64, false, HH); break;                       \
         }                                                                                      \
     } while (0)
 #define QPSK_LAUNCH_MODE(MM) QPSK_LAUNCH_SHAPES(MM, false)

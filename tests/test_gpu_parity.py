@@ -307,45 +307,6 @@ def test_head_prepass_c4_shards(nch, monkeypatch):
     _vs_oracle(x)
 
 
-@pytest.mark.parametrize("width", ["32", "64"])
-def test_pair_back(width, monkeypatch):
-    """Pair-of-lanes backs (QPSK_QUAD=2, back_frame_pair): lane c of a pair
-    does the work of quad lanes c and 3 - c (columns 1 + c and 4 - c, rows c
-    and 3 - c), 32 channels per back wave, W / 32 back waves per frame chain.
-    Ragged batches -- 345 channels at W = 64 (the last workgroup's first
-    block holds 25 channels, its second none), 365 (13 in the second block),
-    and at W = 32 a last workgroup of 25 -- with silent, saturated and
-    constant channels; every output exact."""
-    monkeypatch.setenv("QPSK_WIDTH", width)
-    monkeypatch.setenv("QPSK_QUAD", "2")
-    _vs_oracle(oracle.synth(97, 365, 9, 5.0))
-    x = oracle.synth(98, 345, 15, 4.0)
-    x[3] = 0
-    x[17] = 32767
-    x[18] = -32768
-    x[40, 2:5] = 0
-    x[77, :, ::2] = 12345
-    _vs_oracle(x)
-
-
-@pytest.mark.parametrize("ebn0", [1000.0, 0.0])
-def test_pair_back_noise_and_exact_division(ebn0, monkeypatch):
-    """Pair backs on noiseless and 0 dB channels, and with QPSK_FORCE_EXACT
-    (the IEEE-division retrain of a whole pair wave)."""
-    monkeypatch.setenv("QPSK_WIDTH", "64")
-    monkeypatch.setenv("QPSK_QUAD", "2")
-    _vs_oracle(oracle.synth(71, 160, 9, ebn0))
-    monkeypatch.setenv("QPSK_FORCE_EXACT", "1")
-    _vs_oracle(oracle.synth(72, 100, 8, ebn0))
-
-
-def test_pair_back_c4_shard(monkeypatch):
-    """Pair backs at the C4 N = 4 shard (16,384 channels x 32 frames, AWGN,
-    channels [16384, 32768) of the batch)."""
-    monkeypatch.setenv("QPSK_QUAD", "2")
-    _vs_oracle(oracle.synth(81, 16384, 32, 6.0, c0=16384))
-
-
 @pytest.mark.parametrize("ebn0", [1000.0, 6.0, 0.0])
 def test_quad_back_edges_and_noise(ebn0, monkeypatch):
     """The quad-per-channel back on saturated, zero and constant channels next
