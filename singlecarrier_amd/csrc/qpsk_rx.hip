@@ -70,6 +70,13 @@ constexpr int kDec = 296;
 #ifndef QPSK_HUNT_FILTER
 #define QPSK_HUNT_FILTER 1   // 1: bf16 first pass, exact chain only when the argmax is in doubt (qpsk_hunt.h)
 #endif
+#ifndef QPSK_DYNPRIO
+// dynamic issue priority of the dual-chain back waves (rx_kernel): they train
+// at the highest priority unless another back wave waits for its fronts.
+// 1: quad-back shapes (-1.5% at 8,192 channels, -4% at 4,096; lane backs +1..4%:
+// profiles/r03_dynprio_ab.txt); 0: off; 2: every dual-chain shape (A/B knob)
+#define QPSK_DYNPRIO 1
+#endif
 
 constexpr int kM1 = 1240;
 template <int MODE> struct Cfg;
@@ -828,11 +835,12 @@ constexpr int kDebugStall = 128;  // roles bit: force one progress wait past its
 // (The window load one step ahead stays: a 4-step ring loaded an iteration
 // ahead, as qtrain's, changes this loop's schedule to one with ~50 s_nop per
 // step in the 4x2 kernel.)
-template <bool EXACT>
-__device__ __forceinline__ int train(Kal& k, f2 (&x)[5], const f2* wp2, bool& bad) {
+template <bool EXACT, typename PollFn>
+__device__ __forceinline__ int train(Kal& k, f2 (&x)[5], const f2* wp2, bool& bad, PollFn poll) {
     int matches = 0;
 #pragma unroll 4
     for (int i = 0; i < QK_NPRE; i++) {
+        if ((i & 3) == 0) poll();                  // every 4 steps (dynamic priority)
         const f2 nx = wp2[i + 6];                  // slot i+6 (next step)
         const unsigned long long m = i < 64 ? kPreLo : kPreHi;
         const float ref = ((m >> (i & 63)) & 1ull) ? 1.0f : -1.0f;
@@ -853,9 +861,10 @@ __device__ __forceinline__ int train(Kal& k, f2 (&x)[5], const f2* wp2, bool& ba
 // dec[mi .. mi+162]; read two slots (16 B) every two steps.
 // get_rt() yields rx_timing of frame n; it is called only after the training,
 // so the dual-chain kernel can wait for the previous frame's decision there.
-template <typename RtFn>
+template <typename RtFn, typename PollFn>
 __device__ __forceinline__ void back_frame(const RxArgs& a, int ch, bool live, int n, int mi,
-                                           RtFn get_rt, const float2* win, int* rt_next) {
+                                           RtFn get_rt, const float2* win, int* rt_next,
+                                           PollFn poll) {
     const float4* wp = reinterpret_cast<const float4*>(win);
     Kal k = kal_reset();
     f2 x[5];
@@ -863,11 +872,11 @@ __device__ __forceinline__ void back_frame(const RxArgs& a, int ch, bool live, i
     // equalize(): 128 x train_eq (src/qpsk.c:111-123, src/equalizer.c:45-58)
     const f2* wp2 = reinterpret_cast<const f2*>(win);
     bool bad = (a.roles & kForceExact) != 0;
-    int matches = train<false>(k, x, wp2, bad);
+    int matches = train<false>(k, x, wp2, bad, poll);
     if (__builtin_expect(__ballot(bad) != 0ull, 0)) {   // recompute the frame exactly
         k = kal_reset();
         load_x0(wp, x);
-        matches = train<true>(k, x, wp2, bad);
+        matches = train<true>(k, x, wp2, bad, poll);
     }
     const bool valid = live && matches > QK_MATCH_MIN;   // src/qpsk.c:196
     const size_t cf = (size_t)ch * a.F + n;
@@ -1074,13 +1083,14 @@ __device__ __forceinline__ void qload_x0(const f2* wp2, int c, f2 (&X)[5]) {
 // steps, ~3k cycles) ahead: a load issued one step ahead waited out most of an
 // L2 round trip every step.  wl[s] = x[c+1] of step s; the reads run to step
 // 135, inside the 168-slot window row.
-template <bool EXACT>
-__device__ __forceinline__ int qtrain(QKal& k, f2 (&X)[5], const f2* wl, int c, bool& bad) {
+template <bool EXACT, typename PollFn>
+__device__ __forceinline__ int qtrain(QKal& k, f2 (&X)[5], const f2* wl, int c, bool& bad, PollFn poll) {
     int matches = 0;
     f2 B[4];
 #pragma unroll
     for (int t = 0; t < 4; t++) B[t] = wl[t + 1];
     for (int i = 0; i < QK_NPRE; i += 4) {
+        poll();   // dynamic priority (rx_kernel kDyn)
         f2 Bn[4];
 #pragma unroll
         for (int t = 0; t < 4; t++) Bn[t] = wl[i + 5 + t];
@@ -1103,9 +1113,10 @@ __device__ __forceinline__ int qtrain(QKal& k, f2 (&X)[5], const f2* wl, int c, 
 
 // back_frame() for a quad per channel: every lane of the quad has the same
 // matches / valid / rt; the quad's lane 0 writes the per-channel outputs.
-template <typename RtFn>
+template <typename RtFn, typename PollFn>
 __device__ __forceinline__ void back_frame_quad(const RxArgs& a, int ch, bool live, int n, int mi,
-                                                RtFn get_rt, const float2* win, int* rt_next) {
+                                                RtFn get_rt, const float2* win, int* rt_next,
+                                                PollFn poll) {
     const int c = lane_id() & 3;
     const bool lead = c == 0;
     const f2* wp2 = reinterpret_cast<const f2*>(win);
@@ -1113,11 +1124,11 @@ __device__ __forceinline__ void back_frame_quad(const RxArgs& a, int ch, bool li
     f2 X[5];
     qload_x0(wp2, c, X);
     bool bad = (a.roles & kForceExact) != 0;
-    int matches = qtrain<false>(k, X, wp2 + c + 2, c, bad);
+    int matches = qtrain<false>(k, X, wp2 + c + 2, c, bad, poll);
     if (__builtin_expect(__ballot(bad) != 0ull, 0)) {   // recompute the frame exactly
         k = qkal_reset();
         qload_x0(wp2, c, X);
-        matches = qtrain<true>(k, X, wp2 + c + 2, c, bad);
+        matches = qtrain<true>(k, X, wp2 + c + 2, c, bad, poll);
     }
     const bool valid = live && matches > QK_MATCH_MIN;   // src/qpsk.c:196
     const size_t cf = (size_t)ch * a.F + n;
@@ -1311,6 +1322,7 @@ __global__ void __launch_bounds__(64 * (kBackWavesOf<G, FP, MODE, DUAL, W, QUAD>
     constexpr int kGroups = G, kFrontPer = FP;
     constexpr int kBackWaves = kBackWavesOf<G, FP, MODE, DUAL, W, QUAD>;
     constexpr int kChainWaves = QUAD ? W / 16 : 1;     // back waves per frame chain and group
+    constexpr bool kDyn = DUAL && (QPSK_DYNPRIO == 2 || (QPSK_DYNPRIO == 1 && QUAD));
     constexpr int kFrontCh = W / kFrontPer;            // channels per front wave
     constexpr int kFrontWaves = kGroups * kFrontPer;
     constexpr int kBlock = 64 * (kBackWaves + kFrontWaves);
@@ -1330,6 +1342,7 @@ __global__ void __launch_bounds__(64 * (kBackWavesOf<G, FP, MODE, DUAL, W, QUAD>
     // block per back wave of a chain)
     __shared__ int bseq[kGroups][2][kChainWaves], fcnt[kGroups][2][kChainWaves];
     __shared__ int dead_s;                               // DUAL: a wait of this workgroup timed out
+    __shared__ int nwait_s;                              // kDyn: back waves waiting for their fronts
     const int lane = threadIdx.x & 63;
     // wave-uniform by construction; readfirstlane tells the compiler, so every
     // per-wave index and pointer below lives in SGPRs
@@ -1354,7 +1367,7 @@ __global__ void __launch_bounds__(64 * (kBackWavesOf<G, FP, MODE, DUAL, W, QUAD>
         }
     }
     if (threadIdx.x < 2 * kGroups * kChainWaves) (&bseq[0][0][0])[threadIdx.x] = (&fcnt[0][0][0])[threadIdx.x] = 0;
-    if (threadIdx.x == 0) dead_s = 0;
+    if (threadIdx.x == 0) dead_s = nwait_s = 0;
     __syncthreads();
     if constexpr (DUAL) {
         // Channel blocks: a group's channels split into one block per back wave
@@ -1384,7 +1397,17 @@ __global__ void __launch_bounds__(64 * (kBackWavesOf<G, FP, MODE, DUAL, W, QUAD>
             const int idx = kBlkCh * b + (own ? sub : 0);
             const int ch = (grp0 + gi) * W + idx;
             const bool live = own && ch < a.nch;
-            if (((a.roles >> 4) & 3) == 2) __builtin_amdgcn_s_setprio(2);
+            if (kDyn || ((a.roles >> 4) & 3) == 2) __builtin_amdgcn_s_setprio(2);
+            // kDyn (QPSK_DYNPRIO): every 4 training steps, drop to the lowest
+            // issue priority while another back wave waits for its fronts, else the highest
+            auto poll = [&] {
+                if constexpr (kDyn) {
+                    const int w = __builtin_amdgcn_readfirstlane(
+                        __hip_atomic_load(&nwait_s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+                    if (w > 0) __builtin_amdgcn_s_setprio(0);
+                    else __builtin_amdgcn_s_setprio(2);
+                }
+            };
             // tests (roles bit kDebugStall): one wait that cannot end, on the
             // first back wave of workgroup 0, with a short bound
             if ((a.roles & kDebugStall) && blockIdx.x == 0 && wave == 0)
@@ -1395,7 +1418,24 @@ __global__ void __launch_bounds__(64 * (kBackWavesOf<G, FP, MODE, DUAL, W, QUAD>
             for (int n = wave & 1; n < a.F; n += 2) {
                 const int p = n & 1;
                 // front(n-1) done by every front wave for this block: window n and mi_n
-                if (n > 0) spin_wait(&fcnt[gi][p ^ 1][b], kFrontPer * ((n - 1) / 2 + 1), a.err, &dead_s);
+                if (n > 0) {
+                    int* const fc = &fcnt[gi][p ^ 1][b];
+                    const int need = kFrontPer * ((n - 1) / 2 + 1);
+                    if constexpr (kDyn) {
+                        const bool waits = __builtin_amdgcn_readfirstlane(__hip_atomic_load(
+                                               fc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < need;
+                        if (waits) {   // wait at the lowest priority; poll() resets it
+                            __builtin_amdgcn_s_setprio(0);
+                            if (lane == 0)
+                                __hip_atomic_fetch_add(&nwait_s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        }
+                        spin_wait(fc, need, a.err, &dead_s);
+                        if (waits && lane == 0)
+                            __hip_atomic_fetch_add(&nwait_s, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    } else {
+                        spin_wait(fc, need, a.err, &dead_s);
+                    }
+                }
                 STAMP(14);
                 const int mi = mi_s[gi][p][idx];
                 auto get_rt = [&] {   // rx_timing of frame n = the decision of frame n-1
@@ -1407,9 +1447,9 @@ __global__ void __launch_bounds__(64 * (kBackWavesOf<G, FP, MODE, DUAL, W, QUAD>
                 const float2* wn = win_of(a, a.g0 + (unsigned)n) + (size_t)(live ? ch : 0) * kWinStride;
                 int* rtn = own ? &rt_s[gi][p ^ 1][idx] : nullptr;
                 if constexpr (QUAD)
-                    back_frame_quad(a, live ? ch : 0, live, n, mi, get_rt, wn, rtn);
+                    back_frame_quad(a, live ? ch : 0, live, n, mi, get_rt, wn, rtn, poll);
                 else
-                    back_frame(a, live ? ch : 0, live, n, mi, get_rt, wn, rtn);
+                    back_frame(a, live ? ch : 0, live, n, mi, get_rt, wn, rtn, poll);
                 signal_add(&bseq[gi][p][b], 1, lane);
                 STAMP(13);
             }
@@ -1433,7 +1473,8 @@ __global__ void __launch_bounds__(64 * (kBackWavesOf<G, FP, MODE, DUAL, W, QUAD>
             auto blive = [&](int bb) { return max(0, min(mych, a.nch - bch0(bb))); };
             float2* M = Ms[f];
             int pf[kPf<DM>];
-            if (((a.roles >> 4) & 3) == 1) __builtin_amdgcn_s_setprio(2);
+            if (kDyn) __builtin_amdgcn_s_setprio(1);
+            else if (((a.roles >> 4) & 3) == 1) __builtin_amdgcn_s_setprio(2);
             if (blive(0) > 0) prefetch<DM>(srcs(a, bch0(0), 0), lane, pf);
             // diagnostic stamps (QPSK_STAMPS): 7 wait for the backs, 0 mix,
             // 1 window store + prefetch, 8-12 front_channel phases, 6 its tail,
@@ -1513,7 +1554,7 @@ __global__ void __launch_bounds__(64 * (kBackWavesOf<G, FP, MODE, DUAL, W, QUAD>
                 const int rt = rt_s[gi][p][lane];
                 back_frame(a, live ? ch : 0, live, n, mi_s[gi][p][lane], [=] { return rt; },
                            win_of(a, a.g0 + (unsigned)n) + (size_t)(live ? ch : 0) * kWinStride,
-                           &rt_s[gi][p ^ 1][lane]);
+                           &rt_s[gi][p ^ 1][lane], [] {});
             }
             else
                 rt_s[gi][p ^ 1][lane] = rt_s[gi][p][lane];
