@@ -77,12 +77,6 @@ constexpr int kDec = 296;
 // profiles/r03_dynprio_ab.txt); 0: off; 2: every dual-chain shape (A/B knob)
 #define QPSK_DYNPRIO 1
 #endif
-#ifndef QPSK_DYNLOW
-#define QPSK_DYNLOW 0    // back priority while another back wave waits for its fronts (A/B knob: 0, 1)
-#endif
-#ifndef QPSK_DYNPOLL
-#define QPSK_DYNPOLL 4   // quad training steps between priority updates (A/B knob: 1, 2, 4)
-#endif
 
 constexpr int kM1 = 1240;
 template <int MODE> struct Cfg;
@@ -1096,14 +1090,12 @@ __device__ __forceinline__ int qtrain(QKal& k, f2 (&X)[5], const f2* wl, int c, 
 #pragma unroll
     for (int t = 0; t < 4; t++) B[t] = wl[t + 1];
     for (int i = 0; i < QK_NPRE; i += 4) {
-        if constexpr (QPSK_DYNPOLL >= 4) poll();   // dynamic priority (rx_kernel kDyn)
+        poll();   // dynamic priority (rx_kernel kDyn)
         f2 Bn[4];
 #pragma unroll
         for (int t = 0; t < 4; t++) Bn[t] = wl[i + 5 + t];
 #pragma unroll
         for (int t = 0; t < 4; t++) {
-            if constexpr (QPSK_DYNPOLL < 4)
-                if (t % QPSK_DYNPOLL == 0) poll();
             const int st = i + t;
             const unsigned long long m = st < 64 ? kPreLo : kPreHi;
             const float ref = ((m >> (st & 63)) & 1ull) ? 1.0f : -1.0f;
@@ -1412,7 +1404,7 @@ __global__ void __launch_bounds__(64 * (kBackWavesOf<G, FP, MODE, DUAL, W, QUAD>
                 if constexpr (kDyn) {
                     const int w = __builtin_amdgcn_readfirstlane(
                         __hip_atomic_load(&nwait_s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-                    if (w > 0) __builtin_amdgcn_s_setprio(QPSK_DYNLOW);
+                    if (w > 0) __builtin_amdgcn_s_setprio(0);
                     else __builtin_amdgcn_s_setprio(2);
                 }
             };
