@@ -54,8 +54,9 @@ out = {
     "back_cycles_per_frame": {"work (13)": round(v[13] / bf), "wait fronts (14)": round(v[14] / bf),
                               "wait other chain (15)": round(v[15] / bf)},
     "front_cycles_per_frame": {"wait backs (7)": round(v[7] / ff), "signal (5)": round(v[5] / ff),
-                               "channels (0+1+6)": round((v[0] + v[1] + v[6]) / ff)},
-    "front_cycles_per_channel": {"mix (0)": round(v[0] / fc), "store+prefetch (1)": round(v[1] / fc),
+                               "channels (0+1+4+6)": round((v[0] + v[1] + v[4] + v[6]) / ff)},
+    "front_cycles_per_channel": {"mix (0)": round(v[0] / fc), "window store (4)": round(v[4] / fc),
+                                 "prefetch+sync (1)": round(v[1] / fc),
                                  "front_channel+tail (6)": round(v[6] / fc),
                                  "FIR D (8)": round(v[8] / fc), "FIR head (9)": round(v[9] / fc),
                                  "T image (10)": round(v[10] / fc), "MFMA (11)": round(v[11] / fc),

@@ -235,22 +235,32 @@ __device__ __forceinline__ int item(int lane, int& t) {
     return -1;
 }
 
-template <int MODE, int i>
+// CG: the three frames are consecutive rows of `in` (frame n >= 2): items 0
+// and 10 (MODE 0), which take each lane's sample from one of two frames, are
+// then addressed from one wave-uniform base with a 32-bit lane offset instead
+// of a per-lane 64-bit pointer, which the quad-back kernels kept live across
+// the channel loop and spilled; its reload waited for every load in flight,
+// this prefetch included (profiles/r03_prefetch_ab.txt)
+template <int MODE, int i, bool CG>
 __device__ __forceinline__ void load_item(const Src& s, int lane, int& r) {
     int t;
     const int f = item<MODE, i>(lane, t);
-    if (f >= 0) r = *reinterpret_cast<const int*>((f == 0 ? s.xm2 : f == 1 ? s.xm1 : s.x0) + t);
+    if constexpr (CG) {
+        if (f >= 0) r = *reinterpret_cast<const int*>(s.xm2 + (unsigned)(f * QK_FRAME + t));
+    } else {
+        if (f >= 0) r = *reinterpret_cast<const int*>((f == 0 ? s.xm2 : f == 1 ? s.xm1 : s.x0) + t);
+    }
 }
 
-template <int MODE, int... I>
+template <int MODE, bool CG, int... I>
 __device__ __forceinline__ void prefetch_seq(const Src& s, int lane, int (&r)[kPf<MODE>],
                                              std::integer_sequence<int, I...>) {
-    (load_item<MODE, I>(s, lane, r[I]), ...);
+    (load_item<MODE, I, CG>(s, lane, r[I]), ...);
 }
 
-template <int MODE>
+template <int MODE, bool CG = false>
 __device__ __forceinline__ void prefetch(const Src& s, int lane, int (&r)[kPf<MODE>]) {
-    prefetch_seq<MODE>(s, lane, r, std::make_integer_sequence<int, kPf<MODE>>{});
+    prefetch_seq<MODE, CG>(s, lane, r, std::make_integer_sequence<int, kPf<MODE>>{});
 }
 
 // src/qpsk.c:139-144 as (-1)^G * P[t] * (x * 2^-14), two samples per item.
@@ -1477,51 +1487,69 @@ __global__ void __launch_bounds__(64 * (kBackWavesOf<G, FP, MODE, DUAL, W, QUAD>
             else if (((a.roles >> 4) & 3) == 1) __builtin_amdgcn_s_setprio(2);
             if (blive(0) > 0) prefetch<DM>(srcs(a, bch0(0), 0), lane, pf);
             // diagnostic stamps (QPSK_STAMPS): 7 wait for the backs, 0 mix,
-            // 1 window store + prefetch, 8-12 front_channel phases, 6 its tail,
+            // 4 window store, 1 prefetch, 8-12 front_channel phases, 6 its tail,
             // 5 signal
             STAMP_DECL
             int k = 0;   // channels done, for the dec buffer ring
-            for (int n = 0; n < a.F; n++) {
-                const int p = n & 1;
-                const unsigned g = a.g0 + (unsigned)n;
-                float2* wout = win_of(a, g + 1u);
-                for (int bb = 0; bb < kChainWaves; bb++) {
-                    // back(n-1) of this block done: rx_timing of frame n, and
-                    // window n+1's buffer (window n-1) and mi_{n-1} are free
-                    if (n > 0) spin_wait(&bseq[gi][p ^ 1][bb], (n - 1) / 2 + 1, a.err, &dead_s);
-                    STAMP(7);
-                    const int c0 = bch0(bb), nl = blive(bb);
-                    const int i0 = kBlkCh * bb + cbeg;
-                    int pmi = 0;
-                    for (int c = 0; c < nl; c++, k++) {
-                        const int ch = c0 + c;
-                        float2* dcur = decs[f][k % kDecBuf];
-                        mix<DM>(lane, pf, g, P, M);
-                        STAMP(0);
-                        if (c > 0) store_window(lane, pmi, decs[f][(k - 1) % kDecBuf], wout + (size_t)(ch - 1) * kWinStride);
-                        {   // the next channel: of this block, the next live block, or frame n+1
-                            int nb = bb, nc = c + 1, nn = n;
-                            if (nc >= nl) {
-                                nc = 0;
-                                nb = bb + 1;
-                                while (nb < kChainWaves && blive(nb) == 0) nb++;
-                                if (nb == kChainWaves) { nb = 0; nn = n + 1; }
-                            }
-                            if (nn < a.F) prefetch<DM>(srcs(a, bch0(nb) + nc, nn), lane, pf);
-                        }
-                        wave_lds_sync();
-                        STAMP(1);
-                        pmi = front_channel<MODE, HP>(lane, rt_s[gi][p][i0 + c], M, dcur, BT,
-                                                      a.heads + ((size_t)ch * a.F + n) * kHeadOut FACC_ARG);
-                        if (lane == 0) mi_s[gi][p ^ 1][i0 + c] = pmi;
-                        if (c + 1 == nl) store_window(lane, pmi, dcur, wout + (size_t)ch * kWinStride);
-                        wave_lds_sync();
-                        STAMP(6);
-                    }
-                    signal_add(&fcnt[gi][p][bb], 1, lane);
-                    STAMP(5);
-                }
+// One frame n of a dual-chain front wave's channels.  CG: frame n >= 2, so
+// every prefetch reads consecutive rows of `in` (prefetch<.., true>, see
+// load_item); the quad-back kernels peel frames 0 and 1 off for it (in the
+// lane-back kernels the single loop keeps their code unchanged).
+#define QPSK_DUAL_FRONT_FRAME(CG)                                                                              \
+    do {                                                                                                       \
+        const int p = n & 1;                                                                                   \
+        const unsigned g = a.g0 + (unsigned)n;                                                                 \
+        float2* wout = win_of(a, g + 1u);                                                                      \
+        for (int bb = 0; bb < kChainWaves; bb++) {                                                             \
+            /* back(n-1) of this block done: rx_timing of frame n, and */                                      \
+            /* window n+1's buffer (window n-1) and mi_{n-1} are free */                                       \
+            if (n > 0) spin_wait(&bseq[gi][p ^ 1][bb], (n - 1) / 2 + 1, a.err, &dead_s);                       \
+            STAMP(7);                                                                                          \
+            const int c0 = bch0(bb), nl = blive(bb);                                                           \
+            const int i0 = kBlkCh * bb + cbeg;                                                                 \
+            int pmi = 0;                                                                                       \
+            for (int c = 0; c < nl; c++, k++) {                                                                \
+                const int ch = c0 + c;                                                                         \
+                float2* dcur = decs[f][k % kDecBuf];                                                           \
+                mix<DM>(lane, pf, g, P, M);                                                                    \
+                STAMP(0);                                                                                      \
+                if (c > 0)                                                                                     \
+                    store_window(lane, pmi, decs[f][(k - 1) % kDecBuf], wout + (size_t)(ch - 1) * kWinStride); \
+                STAMP(4);                                                                                      \
+                {   /* the next channel: of this block, the next live block, or frame n+1 */                   \
+                    int nb = bb, nc = c + 1, nn = n;                                                           \
+                    if (nc >= nl) {                                                                            \
+                        nc = 0;                                                                                \
+                        nb = bb + 1;                                                                           \
+                        while (nb < kChainWaves && blive(nb) == 0) nb++;                                       \
+                        if (nb == kChainWaves) { nb = 0; nn = n + 1; }                                         \
+                    }                                                                                          \
+                    if (nn < a.F) prefetch<DM, CG>(srcs(a, bch0(nb) + nc, nn), lane, pf);                      \
+                }                                                                                              \
+                wave_lds_sync();                                                                               \
+                STAMP(1);                                                                                      \
+                pmi = front_channel<MODE, HP>(lane, rt_s[gi][p][i0 + c], M, dcur, BT,                          \
+                                              a.heads + ((size_t)ch * a.F + n) * kHeadOut FACC_ARG);           \
+                if (lane == 0) mi_s[gi][p ^ 1][i0 + c] = pmi;                                                  \
+                if (c + 1 == nl) store_window(lane, pmi, dcur, wout + (size_t)ch * kWinStride);                \
+                wave_lds_sync();                                                                               \
+                STAMP(6);                                                                                      \
+            }                                                                                                  \
+            signal_add(&fcnt[gi][p][bb], 1, lane);                                                             \
+            STAMP(5);                                                                                          \
+        }                                                                                                      \
+    } while (0)
+            if constexpr (QUAD) {
+                auto frame_iter = [&](auto cg, int n) {
+                    constexpr bool CG = decltype(cg)::value;
+                    QPSK_DUAL_FRONT_FRAME(CG);
+                };
+                for (int n = 0; n < a.F && n < 2; n++) frame_iter(std::false_type{}, n);
+                for (int n = 2; n < a.F; n++) frame_iter(std::true_type{}, n);
+            } else {
+                for (int n = 0; n < a.F; n++) QPSK_DUAL_FRONT_FRAME(false);
             }
+#undef QPSK_DUAL_FRONT_FRAME
             STAMP_FLUSH();
             for (int bb = 0; bb < kChainWaves; bb++)
                 carry_history<DM>(a.in, a.hist, a.F, bch0(bb), blive(bb), lane);
