@@ -99,14 +99,16 @@ def free_port() -> int:
     return port
 
 
-def launch(nproc: int, argv, script: str = None, env=None, poll_s: float = 0.2) -> int:
+def launch(nproc: int, argv, script: str = None, env=None, poll_s: float = 0.2,
+           grace_s: float = 10.0) -> int:
     """Run `script argv` as `nproc` ranks (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_*
     as torch.distributed.run sets them), one per GPU, and wait for all of
     them.  The launcher itself makes no GPU call (children are started before
     anything here touches HIP, and by Popen, never exec).  Every child is
     watched: the first one to exit non-zero gets its peers terminated (they
     would otherwise block in gloo's rendezvous or barrier until its timeout),
-    and its status is returned; 0 when every rank succeeds."""
+    killed if they are still alive `grace_s` later, and its status is returned
+    (128 + signal for a rank ended by a signal); 0 when every rank succeeds."""
     import subprocess
     script = script or os.path.abspath(__file__)
     port = free_port()
@@ -117,6 +119,7 @@ def launch(nproc: int, argv, script: str = None, env=None, poll_s: float = 0.2) 
                  MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, script, *argv], env=e))
     first_bad = 0
+    killed_at = None                    # when the peers of a failed rank were terminated
     live = list(procs)
     while live:
         for p in list(live):
@@ -125,13 +128,17 @@ def launch(nproc: int, argv, script: str = None, env=None, poll_s: float = 0.2) 
                 continue
             live.remove(p)
             if rc != 0 and first_bad == 0:
-                first_bad = rc
+                # a rank killed by a signal reports -signum: as a shell would, 128 + signum
+                first_bad = rc if rc > 0 else 128 - rc
+                killed_at = time.monotonic()
                 for q in live:          # exact children of this launcher, by handle
                     q.terminate()
+        if live and killed_at is not None and time.monotonic() - killed_at > grace_s:
+            for q in live:              # a peer that ignored SIGTERM
+                q.kill()
+            killed_at = float("inf")
         if live:
             time.sleep(poll_s)
-    for p in procs:
-        p.wait()
     return first_bad
 
 
@@ -197,6 +204,9 @@ def parse(argv=None):
     ap.add_argument("--stream-chunks", type=int, default=12,
                     help="chunks through the streaming-ingest pipeline after timing (0: skip)")
     ap.add_argument("--stream-frames", type=int, default=4, help="frames per stream chunk")
+    ap.add_argument("--frame-latency", type=int, default=512,
+                    help="frames of one synthetic channel timed through the per-frame drop-in "
+                         "qpsk_rx_frame() (rank 0; 0: skip)")
     ap.add_argument("--sweep", action="store_true",
                     help="C5: AWGN Eb/N0 sweep (GPU vs the reference C on host cores)")
     ap.add_argument("--sweep-frames", type=int, default=16)
@@ -342,6 +352,48 @@ def sweep(args):
                       "all_identical_to_reference": all(r["disagree_bits_vs_ref"] == 0 and
                                                        r["disagree_valid_vs_ref"] == 0
                                                        for r in rows)}), flush=True)
+
+
+SAMPLE_MD5 = "b56a4d3609d0312934aaef69903c5298"   # reference output of preamble_qpsk_8k.raw
+
+
+def frame_latency(nframes: int, seed: int) -> dict:
+    """The per-frame drop-in (qpsk_rx_frame, src/qpsk.c:447's call), timed call
+    by call from the host: the sample capture (its 496-byte records must give
+    the reference output file) and a synthetic one-channel stream of `nframes`
+    frames.  Each call is a full GPU round trip (H2D, two launches, D2H, sync):
+    latency-bound, reported next to the reference's time per frame on one core."""
+    L = sc.lib()
+    raw = np.fromfile(os.path.join(ROOT, "tests", "golden", "preamble_qpsk_8k.raw"), dtype="<i2")
+    frames = raw[: len(raw) // FRAME * FRAME].reshape(-1, FRAME)
+    L.qpsk_rx_init()
+    recs = b""
+    bits = np.zeros(496, np.uint8)
+    for fr in frames:
+        bits[:] = 0
+        if L.qpsk_rx_frame(fr.ctypes.data, bits.ctypes.data):
+            recs += bits.tobytes()
+    import hashlib
+    sample_ok = hashlib.md5(recs).hexdigest() == SAMPLE_MD5 and L.qpsk_surface_error() == 0
+    x = np.ascontiguousarray(sc.synth(seed, 1, nframes)[0])
+    L.qpsk_rx_init()
+    for fr in x[:8]:                         # untimed: first-call allocations
+        L.qpsk_rx_frame(fr.ctypes.data, bits.ctypes.data)
+    L.qpsk_rx_init()
+    us = np.empty(nframes)
+    nvalid = 0
+    for i, fr in enumerate(x):
+        t = time.perf_counter_ns()
+        nvalid += L.qpsk_rx_frame(fr.ctypes.data, bits.ctypes.data)
+        us[i] = (time.perf_counter_ns() - t) / 1e3
+    if L.qpsk_surface_error() != 0:
+        raise sc.QpskError(f"qpsk_rx_frame failed: {L.qpsk_surface_error()}")
+    return {"p50_us": round(float(np.percentile(us, 50)), 1),
+            "p99_us": round(float(np.percentile(us, 99)), 1),
+            "mean_us": round(float(us.mean()), 1), "frames": nframes, "valid_frames": nvalid,
+            "sample_file_md5_ok": bool(sample_ok),
+            "what": "qpsk_rx_frame() per call, host wall time, one synthetic channel "
+                    "(include/qpsk_internal.h, one-channel context on device 0)"}
 
 
 def pmc_record(name: str, nch: int, nf: int, mode: str, khash: str, root: str = ROOT):
@@ -578,6 +630,10 @@ def main():
                   "chunk": f"{nch} channels x {fpc} frames", "chunks": args.stream_chunks,
                   "slots": 3}
 
+    drop_in = None
+    if args.frame_latency > 0 and rank == 0 and mode == sc.MODE_REFERENCE:
+        drop_in = frame_latency(args.frame_latency, args.seed)
+
     # CPU baselines, rank 0, after the timed region (the other ranks wait at
     # the final barrier): the C3 workload's channels 0.. regenerated on the host
     cpu = cpu_all = None
@@ -619,6 +675,9 @@ def main():
                              f"this job may use: affinity {host['affinity_cpus']}, cgroup quota "
                              f"{host['cgroup_cpu_quota']}), slowest {tmx:.1f} s", **host}
 
+    if drop_in is not None and cpu is not None:
+        # the reference's time per frame on one core, from the baseline just timed
+        drop_in["reference_us_per_frame"] = round(FRAME / cpu["value"], 1)
     if rank == 0:
         ch_total = total_ch
         out = {
@@ -649,6 +708,7 @@ def main():
             "verified_vs_oracle": all(v is not None and v["ok"] for v in per_rank) if args.verify else None,
             "verified_per_rank": per_rank if args.verify else None,
             "stream_pcie": stream,
+            "drop_in_frame_latency": drop_in,
             "gpus_visible": ndev,
             "shared_gpus": world > ndev,   # a launcher rehearsal: not a scaling figure
         }

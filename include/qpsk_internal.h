@@ -17,25 +17,59 @@
  */
 #pragma once
 
+/* The reference header's includes (headers/qpsk_internal.h:14-21): a caller
+ * written against it may rely on them transitively.  <complex.h> is C only;
+ * a C++ caller gets the same layout through float _Complex. */
 #include <stdbool.h>
+#include <stddef.h>
 #include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <math.h>
+#ifndef __cplusplus
+#include <complex.h>
+#endif
 
 #ifdef __cplusplus
 extern "C" {
 #endif
 
+/* Constants and helpers of headers/qpsk_internal.h:23-75, same names, values
+ * and expression types (CYCLES is an int expression there too). */
 #define FINE_TIMING_OFFSET 3
+#define TX_FILENAME "/tmp/spectrum-filtered.raw"   /* :25, main()'s TX output */
+#define RX_FILENAME "/tmp/databits.txt"            /* :26, main()'s RX records */
+#define EOF_COST_VALUE 5.0f
 #define EQ_LENGTH 5
 #define FS 8000.0f
 #define RS 1600.0f
-#define CYCLES 5
+#define TS (1.0f / RS)
+#define CYCLES (int)(FS / RS)                      /* 5 */
+#define CYCLESF 5
 #define CENTER 1100.0f
 #define NS 8
 #define DATA_SYMBOLS 31
-#define FRAME_SIZE 1880
-#define BITS_PER_FRAME 496
+#define FRAME_SYMBOLS (DATA_SYMBOLS * NS)
+#define DATA_SAMPLES (DATA_SYMBOLS * CYCLES * NS)
+#define DATA_SIZE 1240                             /* DATA_SYMBOLS * NS * CYCLES */
+#define FRAME_SIZE 1880                            /* preamble + DATA_SIZE */
+#define BITS_PER_FRAME 496                         /* DATA_SYMBOLS * 2 * NS */
 #define PREAMBLE_LENGTH 128
-#define PREAMBLE_SIZE (PREAMBLE_LENGTH * CYCLES)
+#define PREAMBLE_SIZE (PREAMBLE_LENGTH * CYCLESF)
+#ifndef M_PI
+#define M_PI 3.14159265358979323846f
+#endif
+#define TAU (2.0f * M_PI)
+#define ROT45 (M_PI / 4.0f)
+#ifndef __cplusplus
+/* e^{+-i x} as cos + i sin (C only: needs complex.h's I) */
+#define cmplx(float_value) (cosf(float_value) + sinf(float_value) * I)
+#define cmplxconj(float_value) (cosf(float_value) + sinf(float_value) * -I)
+#endif
+
+/* receiver state of the reference's driver (:72-75; write-only there) */
+typedef enum { hunt, process } RXState;
 
 /* headers/qpsk_internal.h:79 -- |val|^2 (re*re + im*im) */
 float cnormf(float _Complex val);

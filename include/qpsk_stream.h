@@ -49,7 +49,11 @@ int qpsk_stream_pending(const qpsk_stream *s);
 /* wait for the oldest submitted chunk; *bits / *valid point into its pinned
  * output buffers (layouts as qpsk_rx_batch).  Returns QPSK_ESTALL (qpsk_batch.h)
  * when a device-side progress wait of that chunk's receive ran out: its
- * outputs are then undefined (the chunk counts as retrieved either way). */
+ * outputs are then undefined (the chunk counts as retrieved either way).  The
+ * stall is sticky: every later chunk starts from the per-channel state the
+ * stalled one left, so it is reported QPSK_ESTALL too, until qpsk_rx_reset()
+ * on qpsk_stream_ctx(s); the stall also reaches that context's own
+ * qpsk_rx_sync(). */
 int qpsk_stream_retrieve(qpsk_stream *s, const uint8_t **bits, const uint8_t **valid);
 /* the stream's receiver (e.g. for qpsk_rx_frames / qpsk_rx_reset between streams) */
 struct qpsk_ctx *qpsk_stream_ctx(qpsk_stream *s);

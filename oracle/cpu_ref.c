@@ -267,7 +267,7 @@ static int data_eq(kal_t *k, const float (*x)[2], float soft[2]) {
 static int rx_frame(qc_chan_t *ch, const int16_t in[QC_FRAME], uint8_t bits[QC_BITS],
                     qc_trace_t *tr, float (*dec_out)[2]);
 
-int qc_decision_step;
+_Thread_local int qc_decision_step;
 
 int qc_rx_frame(qc_chan_t *ch, const int16_t in[QC_FRAME], uint8_t bits[QC_BITS],
                 qc_trace_t *tr) {

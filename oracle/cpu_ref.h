@@ -63,8 +63,9 @@ void qc_chan_init(qc_chan_t *ch);
 void qc_chan_init_mode(qc_chan_t *ch, int mode);
 /* Diagnostics (profiles/decision_steps_drv.c): after qc_rx_frame, the first
  * training step at which the frame's validity was certain (matches > 98, or
- * 30 misses); 128 if only the last step decided it.  Not thread-safe. */
-extern int qc_decision_step;
+ * 30 misses); 128 if only the last step decided it.  Per thread (the batch
+ * path runs qc_rx_frame on pthreads). */
+extern _Thread_local int qc_decision_step;
 /* One qpsk_rx_frame() call.  bits[62] written (zero when invalid). */
 int qc_rx_frame(qc_chan_t *ch, const int16_t in[QC_FRAME], uint8_t bits[QC_BITS],
                 qc_trace_t *tr);

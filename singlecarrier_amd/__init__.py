@@ -61,15 +61,17 @@ KERNEL_SOURCES = ("qpsk_rx.hip", "qpsk_hunt.h", "qpsk_rcp.h", "qpsk_consts.h", "
 
 
 def kernel_source_hash(csrc: str = None) -> str:
-    """The hash the Makefile compiles into the library, from the sources in
-    `csrc` (default: this package's csrc/)."""
-    import hashlib
+    """The hash the Makefile compiles into the library (KERNEL_SOURCES, the
+    C-ABI headers they include, the compile flags and the compiler's version),
+    for the sources in `csrc` (default: this package's csrc/).  The Makefile is
+    the one definition: this asks it (make khash)."""
     csrc = csrc or os.path.join(HERE, "csrc")
-    h = hashlib.sha256()
-    for name in KERNEL_SOURCES:
-        with open(os.path.join(csrc, name), "rb") as f:
-            h.update(f.read())
-    return h.hexdigest()[:16]
+    inc = os.path.join(os.path.dirname(HERE), "include")
+    out = subprocess.run(["make", "-s", "--no-print-directory", "-C", csrc, "khash", f"INCDIR={inc}"],
+                         capture_output=True, text=True)
+    if out.returncode != 0:
+        raise QpskError("make khash failed:\n" + out.stderr[-2000:])
+    return out.stdout.strip()
 
 
 def kernel_hash() -> str:

@@ -840,6 +840,9 @@ __device__ __forceinline__ void load_x0(const float4* wp, f2 (&x)[5]) {
 
 constexpr int kForceExact = 64;   // roles bit: take the exact-division path (tests)
 constexpr int kDebugStall = 128;  // roles bit: force one progress wait past its bound (tests)
+constexpr int kFrontIdle = 1 << 20;  // roles bit (QPSK_ABLATE=frontidle, profiling; output invalid):
+                                     // dual-chain fronts skip their channels from frame 2 on, so
+                                     // the back waves train (stale windows) with the SIMDs to themselves
 
 // 128 x train_eq (src/equalizer.c:45-58) from the window; returns matches.
 // (The window load one step ahead stays: a 4-step ring loaded an iteration
@@ -1505,7 +1508,7 @@ __global__ void __launch_bounds__(64 * (kBackWavesOf<G, FP, MODE, DUAL, W, QUAD>
             /* window n+1's buffer (window n-1) and mi_{n-1} are free */                                       \
             if (n > 0) spin_wait(&bseq[gi][p ^ 1][bb], (n - 1) / 2 + 1, a.err, &dead_s);                       \
             STAMP(7);                                                                                          \
-            const int c0 = bch0(bb), nl = blive(bb);                                                           \
+            const int c0 = bch0(bb), nl = ((a.roles & kFrontIdle) && n >= 2) ? 0 : blive(bb);                  \
             const int i0 = kBlkCh * bb + cbeg;                                                                 \
             int pmi = 0;                                                                                       \
             for (int c = 0; c < nl; c++, k++) {                                                                \
@@ -1689,12 +1692,13 @@ struct qpsk_ctx {
     size_t jobs_cap = 0;           // jobs (one per channel-frame of the largest call)
     unsigned* d_njobs = nullptr;   // [2] counters, alternating by call
     uint64_t calls = 0;
-    // staging for the host-memory entry point
-    int16_t* s_in = nullptr;
-    uint8_t* s_bits = nullptr;
-    uint8_t* s_valid = nullptr;
-    int32_t* s_trace = nullptr;
-    float* s_soft = nullptr;
+    // staging for the host-memory entry point (qpsk_rx_batch): one device block
+    // [in | bits | valid | trace | soft] (stage_grow) and, for small calls, a
+    // pinned host image of it, so a call is one H2D and one D2H of pinned
+    // memory (the per-frame drop-in qpsk_rx_frame is such a call)
+    char* s_dev = nullptr;
+    char* s_pin = nullptr;          // pinned, same layout; only while small
+    int* s_pin_err = nullptr;       // pinned: the error word, read after the call
     size_t s_frames = 0;
     // kernel-span accounting: events before rx_kernel, between the kernels, after
     // rx_data_kernel
@@ -1721,6 +1725,8 @@ struct qpsk_ctx {
     bool called = false;        // `done` has been recorded
     float pend_ms[2] = {0.0f, 0.0f};
     int pend_frames = 0;
+    uint64_t epoch = 0;         // qpsk_rx_reset() count (qpsk_rx_epoch)
+    int stall_calls = -1;       // QPSK_DEBUG_STALL=first: the stall only in call 0; -1: every call
 };
 
 extern "C" int qpsk_rx_timing_split(qpsk_ctx* c, float* ms_rx, float* ms_data, int* frames);
@@ -1796,8 +1802,12 @@ extern "C" int qpsk_rx_reset(qpsk_ctx* c) {
     HCHECK(hipStreamSynchronize(c->stream));
     c->frames = 0;
     c->calls = 0;
+    c->epoch++;
     return QPSK_OK;
 }
+
+int* qpsk_rx_err_word(qpsk_ctx* c) { return c ? c->d_err : nullptr; }
+uint64_t qpsk_rx_epoch(const qpsk_ctx* c) { return c ? c->epoch : 0; }
 
 static void ctx_free(qpsk_ctx* c) {
     for (int i = 0; i < qpsk_ctx::kEv; i++)
@@ -1817,11 +1827,9 @@ static void ctx_free(qpsk_ctx* c) {
         (void)hipFree(c->d_mi[p]);
         (void)hipFree(c->d_rt[p]);
     }
-    (void)hipFree(c->s_in);
-    (void)hipFree(c->s_bits);
-    (void)hipFree(c->s_valid);
-    (void)hipFree(c->s_trace);
-    (void)hipFree(c->s_soft);
+    (void)hipFree(c->s_dev);
+    (void)hipHostFree(c->s_pin);
+    (void)hipHostFree(c->s_pin_err);
     if (c->stream) (void)hipStreamDestroy(c->stream);
 }
 
@@ -1879,9 +1887,13 @@ extern "C" qpsk_ctx* qpsk_rx_create_mode(int device, int nch, int mode, int* err
     if (const char* ab = getenv("QPSK_ABLATE")) {   // timing experiments; output invalid
         if (!strcmp(ab, "front")) c->roles = (c->roles & ~3) | 2;
         else if (!strcmp(ab, "back")) c->roles = (c->roles & ~3) | 1;
+        else if (!strcmp(ab, "frontidle")) c->roles |= kFrontIdle;
     }
     if (getenv("QPSK_FORCE_EXACT")) c->roles |= kForceExact;   // tests: exact-division path
-    if (getenv("QPSK_DEBUG_STALL")) c->roles |= kDebugStall;   // tests: the QPSK_ESTALL path
+    if (const char* ds = getenv("QPSK_DEBUG_STALL")) {          // tests: the QPSK_ESTALL path
+        c->roles |= kDebugStall;
+        if (!strcmp(ds, "first")) c->stall_calls = 1;           // only the context's first call
+    }
     if (const char* w = getenv("QPSK_WIDTH")) {
         const int v = atoi(w);
         c->width = (v == 16 || v == 32 || v == 64) ? v : 0;
@@ -2019,7 +2031,8 @@ int qpsk_rx_launch(qpsk_ctx* c, const int16_t* d_in, int F, uint8_t* d_bits, uin
         c->ev_frames[slot] = F;
     }
     const int parity = (int)(c->calls & 1u);
-    const Shape sh = pick_shape(c);
+    Shape sh = pick_shape(c);
+    if (c->stall_calls >= 0 && c->calls >= (uint64_t)c->stall_calls) sh.roles &= ~kDebugStall;
 #define QPSK_LAUNCH(GG, FF, MM, DD, WW, QQ, HH)                                                \
     hipLaunchKernelGGL((rx_kernel<GG, FF, MM, DD, WW, QQ, HH>),                                \
                        dim3((unsigned)((c->nch + (size_t)GG * WW - 1) / ((size_t)GG * WW))),   \
@@ -2144,21 +2157,36 @@ extern "C" int qpsk_rx_timing_collect(qpsk_ctx* c, float* ms, int* frames) {
     return r;
 }
 
+// byte offsets of the staging block for cf channel-frames
+struct Stage {
+    size_t in, bits, valid, trace, soft, end;
+};
+static Stage stage_of(size_t cf) {
+    auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    Stage g;
+    g.in = 0;
+    g.bits = up(sizeof(int16_t) * cf * QK_FRAME);
+    g.valid = g.bits + cf * QK_NBITS;   // bits and valid adjacent: one D2H
+    g.trace = up(g.valid + cf);
+    g.soft = up(g.trace + sizeof(int32_t) * cf * 4);
+    g.end = up(g.soft + sizeof(float) * cf * QK_NDSYM * 2);
+    return g;
+}
+// calls up to this many input bytes stage through pinned memory
+constexpr size_t kPinnedStage = (size_t)8 << 20;
+
 static int stage_grow(qpsk_ctx* c, size_t F) {
     if (F <= c->s_frames) return QPSK_OK;
-    (void)hipFree(c->s_in);
-    (void)hipFree(c->s_bits);
-    (void)hipFree(c->s_valid);
-    (void)hipFree(c->s_trace);
-    (void)hipFree(c->s_soft);
-    c->s_in = nullptr; c->s_bits = nullptr; c->s_valid = nullptr; c->s_trace = nullptr; c->s_soft = nullptr;
+    (void)hipFree(c->s_dev);
+    (void)hipHostFree(c->s_pin);
+    c->s_dev = nullptr;
+    c->s_pin = nullptr;
     c->s_frames = 0;
     const size_t cf = (size_t)c->nch * F;
-    HCHECK(hipMalloc(&c->s_in, sizeof(int16_t) * cf * QK_FRAME));
-    HCHECK(hipMalloc(&c->s_bits, cf * QK_NBITS));
-    HCHECK(hipMalloc(&c->s_valid, cf));
-    HCHECK(hipMalloc(&c->s_trace, sizeof(int32_t) * cf * 4));
-    HCHECK(hipMalloc(&c->s_soft, sizeof(float) * cf * QK_NDSYM * 2));
+    const Stage g = stage_of(cf);
+    HCHECK(hipMalloc(&c->s_dev, g.end));
+    if (g.bits <= kPinnedStage) HCHECK(hipHostMalloc((void**)&c->s_pin, g.end, hipHostMallocDefault));
+    if (!c->s_pin_err) HCHECK(hipHostMalloc((void**)&c->s_pin_err, sizeof(int), hipHostMallocDefault));
     c->s_frames = F;
     return QPSK_OK;
 }
@@ -2171,20 +2199,47 @@ extern "C" int qpsk_rx_batch(qpsk_ctx* c, const int16_t* in, int F, uint8_t* bit
     int r = stage_grow(c, (size_t)F);
     if (r != QPSK_OK) return r;
     const size_t cf = (size_t)c->nch * F;
-    HCHECK(hipMemcpyAsync(c->s_in, in, sizeof(int16_t) * cf * QK_FRAME, hipMemcpyHostToDevice,
-                          c->stream));
-    r = qpsk_rx_batch_device(c, c->s_in, F, c->s_bits, c->s_valid, trace ? c->s_trace : nullptr,
-                             soft ? c->s_soft : nullptr, c->stream);
+    const Stage g = stage_of(cf);
+    char* d = c->s_dev;
+    const bool pin = c->s_pin && g.bits <= kPinnedStage;
+    // pinned: the caller's input is copied into the pinned image (a host memcpy)
+    // and moves in one DMA, outputs come back in one; pageable otherwise
+    char* h = pin ? c->s_pin : nullptr;
+    const size_t nin = sizeof(int16_t) * cf * QK_FRAME, nbv = cf * QK_NBITS + cf;
+    const size_t ntr = sizeof(int32_t) * cf * 4, nso = sizeof(float) * cf * QK_NDSYM * 2;
+    if (pin) memcpy(h + g.in, in, nin);
+    HCHECK(hipMemcpyAsync(d + g.in, pin ? (const void*)(h + g.in) : (const void*)in, nin,
+                          hipMemcpyHostToDevice, c->stream));
+    r = qpsk_rx_batch_device(c, reinterpret_cast<int16_t*>(d + g.in), F,
+                             reinterpret_cast<uint8_t*>(d + g.bits), reinterpret_cast<uint8_t*>(d + g.valid),
+                             trace ? reinterpret_cast<int32_t*>(d + g.trace) : nullptr,
+                             soft ? reinterpret_cast<float*>(d + g.soft) : nullptr, c->stream);
     if (r != QPSK_OK) return r;
-    HCHECK(hipMemcpyAsync(bits, c->s_bits, cf * QK_NBITS, hipMemcpyDeviceToHost, c->stream));
-    HCHECK(hipMemcpyAsync(valid, c->s_valid, cf, hipMemcpyDeviceToHost, c->stream));
-    if (trace)
-        HCHECK(hipMemcpyAsync(trace, c->s_trace, sizeof(int32_t) * cf * 4, hipMemcpyDeviceToHost,
-                              c->stream));
-    if (soft)
-        HCHECK(hipMemcpyAsync(soft, c->s_soft, sizeof(float) * cf * QK_NDSYM * 2,
-                              hipMemcpyDeviceToHost, c->stream));
-    return qpsk_rx_sync(c);
+    if (!pin) {
+        HCHECK(hipMemcpyAsync(bits, d + g.bits, cf * QK_NBITS, hipMemcpyDeviceToHost, c->stream));
+        HCHECK(hipMemcpyAsync(valid, d + g.valid, cf, hipMemcpyDeviceToHost, c->stream));
+        if (trace) HCHECK(hipMemcpyAsync(trace, d + g.trace, ntr, hipMemcpyDeviceToHost, c->stream));
+        if (soft) HCHECK(hipMemcpyAsync(soft, d + g.soft, nso, hipMemcpyDeviceToHost, c->stream));
+        return qpsk_rx_sync(c);
+    }
+    HCHECK(hipMemcpyAsync(h + g.bits, d + g.bits, nbv, hipMemcpyDeviceToHost, c->stream));
+    if (trace) HCHECK(hipMemcpyAsync(h + g.trace, d + g.trace, ntr, hipMemcpyDeviceToHost, c->stream));
+    if (soft) HCHECK(hipMemcpyAsync(h + g.soft, d + g.soft, nso, hipMemcpyDeviceToHost, c->stream));
+    // the error word: every call on this context is ordered on its stream
+    // (qpsk_rx_sync's contract), so reading it behind this call's kernels and
+    // clearing it only when set needs no atomic exchange
+    HCHECK(hipMemcpyAsync(c->s_pin_err, c->d_err, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HCHECK(hipStreamSynchronize(c->stream));
+    memcpy(bits, h + g.bits, cf * QK_NBITS);
+    memcpy(valid, h + g.valid, cf);
+    if (trace) memcpy(trace, h + g.trace, ntr);
+    if (soft) memcpy(soft, h + g.soft, nso);
+    if (*c->s_pin_err != 0) {
+        HCHECK(hipMemsetAsync(c->d_err, 0, sizeof(int), c->stream));
+        HCHECK(hipStreamSynchronize(c->stream));
+        return QPSK_ESTALL;
+    }
+    return QPSK_OK;
 }
 
 #ifdef QPSK_STAMPS

@@ -12,3 +12,10 @@
 // by qpsk_stream_retrieve() for the chunk it happened in.
 int qpsk_rx_launch(qpsk_ctx* c, const int16_t* d_in, int F, uint8_t* d_bits, uint8_t* d_valid,
                    int32_t* d_trace, float* d_soft, hipStream_t s, int* d_err);
+
+// The context's own device error word (qpsk_rx_sync() takes it): a stream
+// slot's stall is OR-ed into it too, so the context sees every stall.
+int* qpsk_rx_err_word(qpsk_ctx* c);
+// Bumped by every qpsk_rx_reset(): a stream keeps reporting a stall for every
+// later chunk until the per-channel state it corrupted has been reset.
+uint64_t qpsk_rx_epoch(const qpsk_ctx* c);

@@ -30,6 +30,11 @@ struct Slot {
 
 int herr(hipError_t e) { return e == hipSuccess ? QPSK_OK : QPSK_EHIP - (int)e; }
 
+// a slot's stall also goes into the context's own error word (qpsk_rx_sync)
+__global__ void err_merge_kernel(int* ctx_err, const int* slot_err) {
+    if (threadIdx.x == 0 && *slot_err != 0) atomicOr(ctx_err, *slot_err);
+}
+
 }  // namespace
 
 struct qpsk_stream {
@@ -38,6 +43,11 @@ struct qpsk_stream {
     hipStream_t s_h2d = nullptr, s_rx = nullptr, s_d2h = nullptr;
     Slot slot[kMaxSlots];
     uint64_t acquired = 0, submitted = 0, retrieved = 0;
+    // A stalled chunk leaves every channel's carried state (rx_timing, windows,
+    // history) undefined, so every later chunk is reported QPSK_ESTALL too,
+    // until qpsk_rx_reset() on the stream's context (a new epoch).
+    bool stalled = false;
+    uint64_t stall_epoch = 0;
 };
 
 #define SCHECK(x) do { const hipError_t e_ = (x); if (e_ != hipSuccess) return herr(e_); } while (0)
@@ -164,6 +174,8 @@ extern "C" int qpsk_stream_submit(qpsk_stream* s) {
     const int r = qpsk_rx_launch(s->rx, q.d_in, s->frames, q.d_bits, q.d_valid, nullptr, nullptr,
                                  s->s_rx, q.d_err);
     if (r != QPSK_OK) return r;
+    hipLaunchKernelGGL(err_merge_kernel, dim3(1), dim3(64), 0, s->s_rx, qpsk_rx_err_word(s->rx), q.d_err);
+    SCHECK(hipGetLastError());
     SCHECK(hipEventRecord(q.received, s->s_rx));
     SCHECK(hipStreamWaitEvent(s->s_d2h, q.received, 0));
     SCHECK(hipMemcpyAsync(q.h_bits, q.d_bits, cf * QK_NBITS, hipMemcpyDeviceToHost, s->s_d2h));
@@ -186,9 +198,16 @@ extern "C" int qpsk_stream_retrieve(qpsk_stream* s, const uint8_t** bits, const 
     *bits = q.h_bits;
     *valid = q.h_valid;
     s->retrieved++;
-    // a progress wait of this chunk's receive ran out: its bits are undefined
-    // (the slot is released all the same; the next chunks report their own)
-    return *q.h_err != 0 ? QPSK_ESTALL : QPSK_OK;
+    // a progress wait of this chunk's receive ran out: its bits are undefined,
+    // and so are those of every later chunk, which start from the state it
+    // left (the slot is released all the same)
+    const uint64_t ep = qpsk_rx_epoch(s->rx);
+    if (s->stalled && ep != s->stall_epoch) s->stalled = false;   // reset since
+    if (*q.h_err != 0) {
+        s->stalled = true;
+        s->stall_epoch = ep;
+    }
+    return s->stalled ? QPSK_ESTALL : QPSK_OK;
 }
 
 extern "C" qpsk_ctx* qpsk_stream_ctx(qpsk_stream* s) { return s ? s->rx : nullptr; }

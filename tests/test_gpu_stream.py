@@ -67,6 +67,38 @@ def test_stream_reports_a_stalled_chunk(monkeypatch):
     assert (np.concatenate(got, axis=1) == oracle.cpu_rx(x)[0]).all()
 
 
+def test_stream_stall_is_sticky_until_reset(monkeypatch):
+    """A stall in the FIRST chunk only (QPSK_DEBUG_STALL=first) leaves every
+    channel's carried state undefined: the clean chunks after it must come
+    back QPSK_ESTALL too, the stream context's qpsk_rx_sync() must see the
+    stall, and after qpsk_rx_reset() the stream must deliver the oracle's bits
+    again."""
+    nch, fpc = 96, 3
+    x = oracle.synth(18, nch, 2 * fpc, 6.0)
+    monkeypatch.setenv("QPSK_DEBUG_STALL", "first")
+    st = sc.Stream(nch, fpc, nslot=3)
+    monkeypatch.delenv("QPSK_DEBUG_STALL")
+    for k in range(3):
+        st.acquire()[...] = x[:, (k % 2) * fpc:(k % 2 + 1) * fpc]
+        st.submit()
+    for _ in range(3):
+        with pytest.raises(sc.QpskError) as ei:
+            st.retrieve()
+        assert ei.value.code == sc.QPSK_ESTALL
+    ctx = sc.lib().qpsk_stream_ctx(st._h)
+    assert sc.lib().qpsk_rx_sync(ctx) == sc.QPSK_ESTALL
+    assert sc.lib().qpsk_rx_reset(ctx) == 0
+    assert sc.lib().qpsk_rx_sync(ctx) == 0
+    got = []
+    for k in range(2):
+        st.acquire()[...] = x[:, k * fpc:(k + 1) * fpc]
+        st.submit()
+    while st.pending:
+        got.append(st.retrieve()[0])
+    st.close()
+    assert (np.concatenate(got, axis=1) == oracle.cpu_rx(x)[0]).all()
+
+
 def test_stream_busy_and_misuse():
     st = sc.Stream(64, 2, nslot=2)
     for _ in range(2):

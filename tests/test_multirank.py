@@ -93,6 +93,25 @@ def test_launcher_stops_the_peers_of_a_failed_rank(tmp_path):
     assert time.perf_counter() - t < 60
 
 
+def test_launcher_kills_a_peer_that_ignores_sigterm(tmp_path):
+    """A peer that ignores SIGTERM is killed after the grace period instead of
+    holding the launcher; a rank ended by a signal reports
+    128 + signum, never a negative status."""
+    import time
+    script = tmp_path / "stubborn.py"
+    script.write_text("import os, signal, sys, time\n"
+                      "signal.signal(signal.SIGTERM, signal.SIG_IGN)\n"
+                      "if os.environ['RANK'] == '1':\n    time.sleep(0.5)\n    sys.exit(4)\n"
+                      "time.sleep(600)\n")
+    t = time.perf_counter()
+    assert bench.launch(2, [], script=str(script), grace_s=1.0) == 4
+    assert time.perf_counter() - t < 30
+    sig = tmp_path / "sig.py"
+    sig.write_text("import os, signal\n"
+                   "if os.environ['RANK'] == '0':\n    os.kill(os.getpid(), signal.SIGKILL)\n")
+    assert bench.launch(2, [], script=str(sig)) == 128 + 9
+
+
 def test_bench_gpus_flag_spawns_ranks():
     """`bench.py --gpus 2` with no WORLD_SIZE runs itself as 2 ranks through
     bench.launch(); --dry-run takes every rank through the host gloo group,
