@@ -349,6 +349,8 @@ def sweep(args):
         print(json.dumps(row), flush=True)
     pool.close()
     print(json.dumps({"sweep": "C5 AWGN Eb/N0", "channels": nch, "frames": nf,
+                      "kernel_hash": sc.kernel_hash(), "reference": "unmodified reference C "
+                      "(oracle/_ref, gcc -O2) on host cores",
                       "all_identical_to_reference": all(r["disagree_bits_vs_ref"] == 0 and
                                                        r["disagree_valid_vs_ref"] == 0
                                                        for r in rows)}), flush=True)
@@ -363,6 +365,7 @@ def frame_latency(nframes: int, seed: int) -> dict:
     the reference output file) and a synthetic one-channel stream of `nframes`
     frames.  Each call is a full GPU round trip (H2D, two launches, D2H, sync):
     latency-bound, reported next to the reference's time per frame on one core."""
+    import singlecarrier_amd as sc
     L = sc.lib()
     raw = np.fromfile(os.path.join(ROOT, "tests", "golden", "preamble_qpsk_8k.raw"), dtype="<i2")
     frames = raw[: len(raw) // FRAME * FRAME].reshape(-1, FRAME)

@@ -90,6 +90,18 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 
 constexpr unsigned long long kPreLo = qhunt::pre_mask(0), kPreHi = qhunt::pre_mask(1);
 
+// the preamble as +-1.0f, read by the training loops as wave-uniform scalar
+// loads (s_load): one per 4 steps instead of bit extraction per step
+struct alignas(16) PreTab {
+    float v[QK_NPRE];
+};
+constexpr PreTab make_pretab() {
+    PreTab t{};
+    for (int i = 0; i < QK_NPRE; i++) t.v[i] = ((i < 64 ? kPreLo >> i : kPreHi >> (i - 64)) & 1ull) ? 1.0f : -1.0f;
+    return t;
+}
+__constant__ PreTab kPreTab = make_pretab();
+
 struct RxArgs {
     const int16_t* in;       // [nch][F][1880]
     int16_t* hist;           // [nch][2][1880]: frames -2, -1 of this call
@@ -675,8 +687,11 @@ __host__ __device__ constexpr int uix(int i, int j) { return j * (j - 1) / 2 + i
 // the gain half of update_eq: kalman_calculate (src/kalman.c:85-141); returns
 // kalman_y (the last 6.22 y).  It never reads eq or the error: the gain
 // recursion of a frame depends only on its window.
+// EXACT = false: `bmax` collects the bit pattern of the step's largest
+// reciprocal operand xs[4] (the callers test bmax <= bits(2^125) once per
+// frame or job: qk_rcp_in_range() for every step, a NaN or -x has larger bits).
 template <bool EXACT>
-__device__ __forceinline__ float kal_gain(Kal& k, const f2 (&x)[5], bool& bad) {
+__device__ __forceinline__ float kal_gain(Kal& k, const f2 (&x)[5], unsigned& bmax) {
     const float E = QK_KAL_E, q = QK_KAL_Q;
     f2 f[5];
     float a[5];
@@ -710,7 +725,11 @@ __device__ __forceinline__ float kal_gain(Kal& k, const f2 (&x)[5], bool& bad) {
 #pragma unroll
         for (int j = 0; j < 5; j++) ys[j] = qk_div_ieee(xs[j]);
     } else {
-        bad |= !qk_rcp_in_range(xs[0], xs[4]);
+        // the one check: xs[0] >= E unless NaN, and a NaN reaches xs[4] too
+        bmax = max(bmax, __float_as_uint(xs[4]));
+        // qk_rcp_fast on pairs: the two Newton FMAs of two divisors packed
+        // (the Newton steps as packed pairs crash ROCm 7.2's greedy register
+        // allocator in several of these kernels: kept scalar)
 #pragma unroll
         for (int j = 0; j < 5; j++) ys[j] = qk_rcp_fast(xs[j]);
     }
@@ -735,8 +754,8 @@ __device__ __forceinline__ float kal_gain(Kal& k, const f2 (&x)[5], bool& bad) {
 // update_eq (src/equalizer.c:25-40): the gain, then error *= kalman_y and
 // eq_i += error * conj(g_i)
 template <bool EXACT>
-__device__ __forceinline__ void update_eq(Kal& k, const f2 (&x)[5], f2 e, bool& bad) {
-    const float y = kal_gain<EXACT>(k, x, bad);
+__device__ __forceinline__ void update_eq(Kal& k, const f2 (&x)[5], f2 e, unsigned& bmax) {
+    const float y = kal_gain<EXACT>(k, x, bmax);
     e = e * y;                                            // error *= kalman_y
 #pragma unroll
     for (int i = 0; i < 5; i++) k.eq[i] = k.eq[i] + cmulc(e, k.g[i]);
@@ -851,6 +870,7 @@ constexpr int kFrontIdle = 1 << 20;  // roles bit (QPSK_ABLATE=frontidle, profil
 template <bool EXACT, typename PollFn>
 __device__ __forceinline__ int train(Kal& k, f2 (&x)[5], const f2* wp2, bool& bad, PollFn poll) {
     int matches = 0;
+    unsigned bmax = 0u;
 #pragma unroll 4
     for (int i = 0; i < QK_NPRE; i++) {
         if ((i & 3) == 0) poll();                  // every 4 steps (dynamic priority)
@@ -861,12 +881,13 @@ __device__ __forceinline__ int train(Kal& k, f2 (&x)[5], const f2* wp2, bool& ba
 #pragma unroll
         for (int t = 0; t < 5; t++) v = v + cmul(x[t], k.eq[t]);
         const float er = ref - v.x;                // conjf(ref - val) = (ref - vr, vi)
-        update_eq<EXACT>(k, x, f2{er, v.y}, bad);
+        update_eq<EXACT>(k, x, f2{er, v.y}, bmax);
         if (er * ref > 0.0f) matches++;
 #pragma unroll
         for (int t = 0; t < 4; t++) x[t] = x[t + 1];
         x[4] = nx;
     }
+    if (!EXACT) bad |= bmax > __float_as_uint(0x1p125f);
     return matches;
 }
 
@@ -966,8 +987,7 @@ struct QKal {
     f2 C[3];      // C[d-2] = u[c+1-d][c+1], d = 2..4
     f2 eqr;       // eq_coeff[c]
     f2 eq4;       // eq_coeff[4] (lane 3)
-    float d0;     // d[0]
-    float dc;     // d[c+1]
+    f2 dd;        // (d[0], d[c+1]): one packed multiply updates both
 };
 
 __device__ __forceinline__ QKal qkal_reset() {   // kalman_reset, src/kalman.c:42-55
@@ -977,43 +997,72 @@ __device__ __forceinline__ QKal qkal_reset() {   // kalman_reset, src/kalman.c:4
 #pragma unroll
     for (int i = 0; i < 3; i++) k.C[i] = f2{0.0f, 0.0f};
     k.eqr = k.eq4 = f2{0.0f, 0.0f};
-    k.d0 = k.dc = 1.0f;
+    k.dd = f2{1.0f, 1.0f};
     return k;
 }
 
+// Packed products with the conj() of the reference folded into a negate
+// modifier (conj never materialised; (-a)*b == -(a*b) exactly):
+// (x.x * d0, (-x.y) * d0) with d0 = dd.x broadcast: conj(x) * d[0]
+__device__ __forceinline__ f2 mul_conj_d0(f2 x, f2 dd) {
+    f2 r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0] neg_hi:[1,0]" : "=v"(r) : "v"(x), "v"(dd));
+    return r;
+}
+// (a.x * b.x, a.y * (-b.y)): a * conj(b) componentwise
+__device__ __forceinline__ f2 mul_conjb(f2 a, f2 b) {
+    f2 r;
+    asm("v_pk_mul_f32 %0, %1, %2 neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+// (f.x * dc, f.y * dc) with dc = dd.y broadcast
+__device__ __forceinline__ f2 mul_dc(f2 f, f2 dd) {
+    f2 r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,1]" : "=v"(r) : "v"(f), "v"(dd));
+    return r;
+}
+
+
 // one train_eq step (src/equalizer.c:45-58 with update_eq/kalman_calculate,
-// exactly update_eq<EXACT>'s operations) on the quad layout.  X[d] = x[c+1-d]
+// exactly update_eq<EXACT>'s operations) on the quad layout.  X0..X4 = x[c+1-d]
 // (x[index+t] of the reference), zero before x[0].  Returns er = Re(error).
+// EXACT = false: `bmax` collects the bit patterns of the step's largest
+// reciprocal operand (xso, lane c: xs[c+1], nondecreasing in j, and >= xs[0]
+// >= E unless NaN); the caller tests bmax <= bits(2^125) once per frame, which
+// is qk_rcp_in_range() for every step (a NaN or -x has larger bits).
 template <bool EXACT>
-__device__ __forceinline__ float qstep(QKal& k, const f2 (&X)[5], float ref, int c, bool& bad) {
+__device__ __forceinline__ float qstep(QKal& k, const f2& X0, const f2& X1, const f2& X2, const f2& X3,
+                                       const f2& X4, float ref, int c, unsigned& bmax) {
     const float E = QK_KAL_E, q = QK_KAL_Q;
     // 1 where row c has column c+d (d = 2, 3, 4), else 0: h of a missing
     // column is multiplied by 0, so the padding entries of R stay +0
     const float m2 = c < 3 ? 1.0f : 0.0f, m3 = c < 2 ? 1.0f : 0.0f, m4 = c < 1 ? 1.0f : 0.0f;
-    // val = sum_t x[t] * eq[t], t = 0..4 in order (src/equalizer.c:49-51)
-    const f2 p = cmul(X[1], k.eqr);       // lane c: x[c] * eq[c]
-    const f2 p4 = cmul(X[0], k.eq4);      // lane 3: x[4] * eq[4]
+    // val = sum_t x[t] * eq[t], t = 0..4 in order (src/equalizer.c:49-51); the
+    // reference's 0 + x[0]*eq[0] only differs from x[0]*eq[0] in the sign of a
+    // zero, which no output observes, so the chain starts with
+    // the broadcast itself
+    const f2 p = cmul(X1, k.eqr);         // lane c: x[c] * eq[c]
+    const f2 p4 = cmul(X0, k.eq4);        // lane 3: x[4] * eq[4]
     // (the empty asm keeps the two components scalar adds, so each folds its
     // DPP source into one v_add_f32_dpp instead of two moves and a packed add)
-    float vr = 0.0f, vi = 0.0f;
+    float vr = qdf<qd::kB0>(p.x), vi = qdf<qd::kB0>(p.y);
 #define QV(CT, P)                                                   \
     vr = vr + qdf<CT>(P.x); vi = vi + qdf<CT>(P.y);                 \
     asm("" : "+v"(vr), "+v"(vi))
-    QV(qd::kB0, p); QV(qd::kB1, p); QV(qd::kB2, p); QV(qd::kB3, p); QV(qd::kB3, p4);
+    QV(qd::kB1, p); QV(qd::kB2, p); QV(qd::kB3, p); QV(qd::kB3, p4);
 #undef QV
     const float er = ref - vr;            // conjf(ref - val) = (ref - vr, vi)
-    // column 0 (every lane): f0 = conj(x0), 6.2
-    const f2 x0 = qd2<qd::kB0>(X[1]);
-    const f2 f0 = conj2(x0);
-    const f2 g0 = f0 * k.d0;                              // 6.4
-    const f2 t0 = g0 * f0;
+    // column 0 (every lane): f0 = conj(x0), 6.2; g0 = f0 * d0, 6.4; t0 = g0 * f0
+    const f2 x0 = qd2<qd::kB0>(X1);
+    const f2 g0 = mul_conj_d0(x0, k.dd);
+    const f2 t0 = mul_conjb(g0, x0);
     const float a0 = E + (t0.x + t0.y);                   // 6.5
     // column c+1: f = u[0][j]*conj(x0) + conj(xj) + sum_{0<i<j} u[i][j]*conj(xi)
-    f2 f = addc(cmulc(k.C[2], X[4]), X[0]);
-    f = f + cmulc(k.C[1], X[3]);
-    f = f + cmulc(k.C[0], X[2]);
-    f = f + cmulc(k.R[0], X[1]);
-    const f2 g = f * k.dc;                                // 6.4
+    f2 f = addc(cmulc(k.C[2], X4), X0);
+    f = f + cmulc(k.C[1], X3);
+    f = f + cmulc(k.C[0], X2);
+    f = f + cmulc(k.R[0], X1);
+    const f2 g = mul_dc(f, k.dd);                         // 6.4
     const f2 t = g * f;
     const float s = t.x + t.y;
     // 6.6 a[j] = a[j-1] + Re(g conj f), the quad's s in column order
@@ -1025,18 +1074,17 @@ __device__ __forceinline__ float qstep(QKal& k, const f2 (&X)[5], float ref, int
     const float ht = a4 * q;
     const float ap = c == 0 ? a0 : c == 1 ? a1 : c == 2 ? a2 : a3;   // a[c]
     const float ao = ap + s;                              // a[c+1], the chain's own add
-    const float xs0 = a0 + ht, xso = ao + ht;
-    float y0, yo;
+    const f2 xs = f2{a0, ao} + f2{ht, ht};               // (xs[0], xs[c+1]), 6.19 / 6.22 operands
+    f2 y;
     if (EXACT) {
-        y0 = qk_div_ieee(xs0);
-        yo = qk_div_ieee(xso);
+        y = f2{qk_div_ieee(xs.x), qk_div_ieee(xs.y)};
     } else {
-        bad |= !qk_rcp_in_range(xs0, xso);   // xs is nondecreasing in j (update_eq)
-        y0 = qk_rcp_fast(xs0);
-        yo = qk_rcp_fast(xso);
+        bmax = max(bmax, __float_as_uint(xs.y));
+        y = f2{qk_rcp_fast(xs.x), qk_rcp_fast(xs.y)};
     }
-    k.d0 = k.d0 * ((hq * (E + ht)) * y0);                 // 6.20
-    k.dc = k.dc * ((hq * (ap + ht)) * yo);                // 6.21, 6.13
+    // 6.20 / 6.21+6.13: d[0] *= (hq * (E + ht)) * y0, d[c+1] *= (hq * (a[c] + ht)) * y[c+1]
+    k.dd = k.dd * ((f2{hq, hq} * (f2{E, ap} + f2{ht, ht})) * y);
+    const float y0 = y.x, yo = y.y;
     // (every DPP move is made unconditionally, then selected: a move inside
     // a conditional would become a branch, the intrinsic being convergent)
     const float yr = qdf<qd::kRot1>(yo);
@@ -1092,35 +1140,39 @@ __device__ __forceinline__ void qload_x0(const f2* wp2, int c, f2 (&X)[5]) {
     for (int d = 0; d < 5; d++) X[d] = d <= c + 1 ? wp2[c + 2 - d] : f2{0.0f, 0.0f};
 }
 
-// Window samples arrive through a 4-step ring loaded one loop iteration (4
-// steps, ~3k cycles) ahead: a load issued one step ahead waited out most of an
-// L2 round trip every step.  wl[s] = x[c+1] of step s; the reads run to step
-// 135, inside the 168-slot window row.
+// The window as a ring of 8 samples per lane, w[s mod 8] = x[c+1] of step s
+// (wl[s]; w of a negative step: X of step 0, zero-padded); step s reads
+// X[d] = w[(s - d) mod 8].  Eight steps per loop iteration, so the ring's
+// roles repeat every iteration and no register moves at the back edge; the
+// sample of step s+4 is loaded right after step s, into the slot step s read
+// last (reads run to step 131, inside the 168-slot window row).
 template <bool EXACT, typename PollFn>
-__device__ __forceinline__ int qtrain(QKal& k, f2 (&X)[5], const f2* wl, int c, bool& bad, PollFn poll) {
+__device__ __forceinline__ int qtrain(QKal& k, const f2 (&X)[5], const f2* wl, int c, bool& bad, PollFn poll) {
     int matches = 0;
-    f2 B[4];
+    unsigned bmax = 0u;
+    f2 w[8];
+    w[0] = X[0];
+    w[7] = X[1];
+    w[6] = X[2];
+    w[5] = X[3];
+    w[4] = X[4];
 #pragma unroll
-    for (int t = 0; t < 4; t++) B[t] = wl[t + 1];
-    for (int i = 0; i < QK_NPRE; i += 4) {
-        poll();   // dynamic priority (rx_kernel kDyn)
-        f2 Bn[4];
+    for (int t = 1; t < 4; t++) w[t] = wl[t];
+    for (int i = 0; i < QK_NPRE; i += 8) {
+        const float4 r0 = *reinterpret_cast<const float4*>(&kPreTab.v[i]);
+        const float4 r1 = *reinterpret_cast<const float4*>(&kPreTab.v[i + 4]);
+        const float ref8[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
 #pragma unroll
-        for (int t = 0; t < 4; t++) Bn[t] = wl[i + 5 + t];
-#pragma unroll
-        for (int t = 0; t < 4; t++) {
-            const int st = i + t;
-            const unsigned long long m = st < 64 ? kPreLo : kPreHi;
-            const float ref = ((m >> (st & 63)) & 1ull) ? 1.0f : -1.0f;
-            const float er = qstep<EXACT>(k, X, ref, c, bad);
-            if (er * ref > 0.0f) matches++;
-#pragma unroll
-            for (int d = 4; d > 0; d--) X[d] = X[d - 1];
-            X[0] = B[t];
+        for (int t = 0; t < 8; t++) {
+            if ((t & 3) == 0) poll();   // every 4 steps (dynamic priority, rx_kernel kDyn)
+            const float ref = ref8[t];
+            const float er = qstep<EXACT>(k, w[t & 7], w[(t + 7) & 7], w[(t + 6) & 7], w[(t + 5) & 7],
+                                          w[(t + 4) & 7], ref, c, bmax);
+            matches += (er * ref > 0.0f) ? 1 : 0;
+            w[(t + 4) & 7] = wl[i + t + 4];   // sample of step i+t+4
         }
-#pragma unroll
-        for (int t = 0; t < 4; t++) B[t] = Bn[t];
     }
+    if (!EXACT) bad |= bmax > __float_as_uint(0x1p125f);
     return matches;
 }
 
@@ -1159,9 +1211,9 @@ __device__ __forceinline__ void back_frame_quad(const RxArgs& a, int ch, bool li
         QU(2, 3, qd::kB2); QU(2, 4, qd::kB2);
         QU(3, 4, qd::kB3);
 #undef QU
-        j.k.d[0] = f2{k.d0, k.d0};
-        const float d1 = qdf<qd::kB0>(k.dc), d2 = qdf<qd::kB1>(k.dc);
-        const float d3 = qdf<qd::kB2>(k.dc), d4 = qdf<qd::kB3>(k.dc);
+        j.k.d[0] = f2{k.dd.x, k.dd.x};
+        const float d1 = qdf<qd::kB0>(k.dd.y), d2 = qdf<qd::kB1>(k.dd.y);
+        const float d3 = qdf<qd::kB2>(k.dd.y), d4 = qdf<qd::kB3>(k.dd.y);
         j.k.d[1] = f2{d1, d1};
         j.k.d[2] = f2{d2, d2};
         j.k.d[3] = f2{d3, d3};
@@ -1213,13 +1265,13 @@ struct JobX {
 #endif
 template <bool EXACT>
 __device__ __forceinline__ void data_step(Kal& k, f2 (&x)[5], f2 nx, int s, unsigned long long& dib,
-                                          float2* so, bool& bad) {
+                                          float2* so, unsigned& bmax) {
     f2 sy = {0.0f, 0.0f};
 #pragma unroll
     for (int t = 0; t < 5; t++) sy = sy + cmulc(x[t], k.eq[t]);
     const int dI = sy.x < 0.0f, dQ = sy.y < 0.0f;
     const f2 cst = {dI ? -1.0f : 1.0f, dQ ? -1.0f : 1.0f};
-    update_eq<EXACT>(k, x, (cst - sy) * 0.1f, bad);
+    update_eq<EXACT>(k, x, (cst - sy) * 0.1f, bmax);
     dib |= (unsigned long long)(dQ | (dI << 1)) << (2 * s);
     if (so) so[s] = make_float2(sy.x, sy.y);
 #pragma unroll
@@ -1231,6 +1283,7 @@ template <bool EXACT>
 __device__ __forceinline__ unsigned long long data_steps(Kal& k, f2 (&x)[5], const JobX xs,
                                                          float2* so, bool& bad) {
     unsigned long long dib = 0;
+    unsigned bmax = 0u;
 #if QPSK_DATA_RING > 1
     // the job's samples arrive from HBM (written ~ms earlier by rx_kernel):
     // each is loaded R steps before it enters x
@@ -1244,13 +1297,14 @@ __device__ __forceinline__ unsigned long long data_steps(Kal& k, f2 (&x)[5], con
         for (int t = 0; t < R; t++) nxt[t] = xs[min(s0 + R + 5 + t, 34)];
 #pragma unroll
         for (int t = 0; t < R; t++)
-            if (s0 + t < QK_NDSYM) data_step<EXACT>(k, x, cur[t], s0 + t, dib, so, bad);
+            if (s0 + t < QK_NDSYM) data_step<EXACT>(k, x, cur[t], s0 + t, dib, so, bmax);
 #pragma unroll
         for (int t = 0; t < R; t++) cur[t] = nxt[t];
     }
 #else
-    for (int s = 0; s < QK_NDSYM; s++) data_step<EXACT>(k, x, xs[min(s + 5, 34)], s, dib, so, bad);
+    for (int s = 0; s < QK_NDSYM; s++) data_step<EXACT>(k, x, xs[min(s + 5, 34)], s, dib, so, bmax);
 #endif
+    if (!EXACT) bad |= bmax > __float_as_uint(0x1p125f);
     return dib;
 }
 
@@ -1726,7 +1780,8 @@ struct qpsk_ctx {
     float pend_ms[2] = {0.0f, 0.0f};
     int pend_frames = 0;
     uint64_t epoch = 0;         // qpsk_rx_reset() count (qpsk_rx_epoch)
-    int stall_calls = -1;       // QPSK_DEBUG_STALL=first: the stall only in call 0; -1: every call
+    int stall_calls = -1;       // QPSK_DEBUG_STALL=first: the stall only in the first launch; -1: every call
+    uint64_t launches = 0;      // calls launched over the context's life (qpsk_rx_reset keeps it)
 };
 
 extern "C" int qpsk_rx_timing_split(qpsk_ctx* c, float* ms_rx, float* ms_data, int* frames);
@@ -2032,7 +2087,7 @@ int qpsk_rx_launch(qpsk_ctx* c, const int16_t* d_in, int F, uint8_t* d_bits, uin
     }
     const int parity = (int)(c->calls & 1u);
     Shape sh = pick_shape(c);
-    if (c->stall_calls >= 0 && c->calls >= (uint64_t)c->stall_calls) sh.roles &= ~kDebugStall;
+    if (c->stall_calls >= 0 && c->launches >= (uint64_t)c->stall_calls) sh.roles &= ~kDebugStall;
 #define QPSK_LAUNCH(GG, FF, MM, DD, WW, QQ, HH)                                                \
     hipLaunchKernelGGL((rx_kernel<GG, FF, MM, DD, WW, QQ, HH>),                                \
                        dim3((unsigned)((c->nch + (size_t)GG * WW - 1) / ((size_t)GG * WW))),   \
@@ -2085,6 +2140,7 @@ int qpsk_rx_launch(qpsk_ctx* c, const int16_t* d_in, int F, uint8_t* d_bits, uin
     c->called = true;
     c->frames += (uint64_t)F;
     c->calls++;
+    c->launches++;
     return QPSK_OK;
 }
 
