@@ -44,7 +44,24 @@ def parse(lines):
         toks = [t.strip() for t in re.split(r",\s*", rest.strip()) if t.strip()]
         toks = [t.split()[0] for t in toks]
         dst, src = [], []
-        if op.startswith("v_") and toks:
+        if op.startswith("v_pk_") and toks:
+            # packed: source i's low register feeds the low result unless
+            # op_sel[i], its high register the high result unless op_sel_hi[i] = 0
+            def bits(name, k, dflt):
+                m = re.search(name + r":\[([0-9,]+)\]", s)
+                v = [int(x) for x in m.group(1).split(",")] if m else []
+                return [v[i] if i < len(v) else dflt for i in range(k)]
+            srcs = toks[1:]
+            osel = bits(r"(?<!_)op_sel", len(srcs), 0)
+            oshi = bits("op_sel_hi", len(srcs), 1)
+            dst = regs(toks[0])
+            for i, t in enumerate(srcs):
+                rr = regs(t)
+                if len(rr) == 2:
+                    src += [rr[1] if osel[i] else rr[0], rr[1] if oshi[i] else rr[0]]
+                else:
+                    src += rr
+        elif op.startswith("v_") and toks:
             if op.startswith(("v_cmp", "v_readfirstlane", "v_readlane")):
                 src = [r for t in toks[1:] for r in regs(t)]
             else:

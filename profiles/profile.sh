@@ -10,7 +10,7 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 # provenance of the profiled kernels (summarize.py -> pmc_*.json -> bench.py)
 python3 -c "import singlecarrier_amd as sc; print(sc.kernel_hash())" > $OUT/kernel_hash.txt
-B="bench.py --steps 5 --warmup 2 --cpu-channels 0 --cpu-all-channels 0 --stream-chunks 0 --verify 0 $*"
+B="bench.py --steps 5 --warmup 2 --cpu-channels 0 --cpu-all-channels 0 --stream-chunks 0 --frame-latency 0 --verify 0 $*"
 run() { # name, rocprof args...
   local name=$1; shift
   timeout -k 10 300 rocprofv3 "$@" --output-format csv -d $OUT/$name -o $name -- python3 $B \

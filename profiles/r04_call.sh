@@ -21,6 +21,7 @@ for what in "$@"; do
     bench) timeout -k 10 400 python bench.py > ${O}_bench.json 2> ${O}_bench.err; check bench $? ;;
     prof)  timeout -k 10 900 bash profiles/profile.sh r04_c${N}; check prof $? ;;
     curve) timeout -k 10 600 bash profiles/ab_shards.sh 1 "65536 32768 16384 8192 4096" singlecarrier_amd/libqpsk_hip.so > ${O}_curve.txt 2>&1; check curve $? ;;
+    sweep) timeout -k 10 1100 python bench.py --sweep --cpu-procs 16 > ${O}_sweep.jsonl 2> ${O}_sweep.err; check sweep $? ;;
     env)   { nproc; cat /sys/fs/cgroup/cpu.max; python3 -c "import os; print(len(os.sched_getaffinity(0)))"; } > ${O}_env.txt 2>&1 ;;
     *) echo "unknown step $what" >&2; exit 2 ;;
   esac

@@ -64,6 +64,12 @@ constexpr int kDec = 296;
 #ifndef QPSK_FB
 #define QPSK_FB 15   // FIR samples per LDS batch (A/B knob)
 #endif
+#ifndef QPSK_RX_ATTR
+#define QPSK_RX_ATTR   // A/B: e.g. __attribute__((amdgpu_num_vgpr(128))) to price a 4-wave budget
+#endif
+#ifndef QPSK_FIR_SB
+#define QPSK_FIR_SB 0   // 1: scheduling barrier after each FIR batch (register pressure A/B knob)
+#endif
 #ifndef QPSK_HUNT_MFMA
 #define QPSK_HUNT_MFMA 1   // 1: hunt on the matrix cores; 0: packed VALU chains (A/B knob)
 #endif
@@ -427,6 +433,9 @@ __device__ __forceinline__ void fir_dec(int lane, int rt, const float2* M, float
                     if (s < 59 && k >= 0 && k < QK_NTAPS) y[m] = y[m] + v[j] * QK_RRC[k];
                 }
             }
+#if QPSK_FIR_SB
+            __builtin_amdgcn_sched_barrier(0);   // keep the next batch's loads behind this one
+#endif
         }
 #pragma unroll
         for (int m = 0; m < 3; m++)
@@ -1379,7 +1388,7 @@ constexpr int kBackWavesOf = DUAL ? 2 * G * (QUAD ? W / 16 : 1) : G;
 //
 // HP: the fronts take F_{n+1} from the head pre-pass (head_kernel, QPSK_HEADPASS).
 template <int G, int FP, int MODE, bool DUAL, int W = QK_GROUP, bool QUAD = false, bool HP = false>
-__global__ void __launch_bounds__(64 * (kBackWavesOf<G, FP, MODE, DUAL, W, QUAD> + G * FP), 3) rx_kernel(
+__global__ void __launch_bounds__(64 * (kBackWavesOf<G, FP, MODE, DUAL, W, QUAD> + G * FP), 3) QPSK_RX_ATTR rx_kernel(
     const int16_t* in, int16_t* hist, const float2* ptab, const unsigned long long* ks,
     float2* win0, float2* win1, int* mi0, int* mi1, int* rt0, int* rt1, uint8_t* bits,
     uint8_t* valid, int32_t* trace, float2* soft, float4* jobs, unsigned* njobs, int nch, int F,
