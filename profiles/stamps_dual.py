@@ -9,8 +9,6 @@ Per back wave and frame it trains: frame work (13: 128 train_eq steps, job,
 outputs), wait for the fronts (14), wait for the other chain's decision (15).
 Per front wave and frame: wait for the backs (7), per channel: mix (0), window
 store + prefetch (1), front_channel + tail (6, of which 8-12 are its phases).
-Speculative fronts (QPSK_SPEC): 7 is the wait for the decision and for every
-front wave's guesses; "spec" counts guessed and redone channels.
 """
 import ctypes as C
 import json
@@ -28,8 +26,6 @@ nf = int(sys.argv[2]) if len(sys.argv) > 2 else 32
 sc.LIB_PATH = os.path.join(ROOT, "singlecarrier_amd", "csrc", "build", "libqpsk_hip_stamps.so")
 lib = sc.lib()
 lib.qpsk_debug_stamps.argtypes = [C.c_void_p, C.c_int]
-lib.qpsk_debug_counts.argtypes = [C.c_void_p, C.c_int]
-cnt = np.zeros(4, np.uint64)
 import torch  # noqa: E402
 
 ncu = torch.cuda.get_device_properties(0).multi_processor_count
@@ -46,11 +42,9 @@ st = np.zeros(16, np.uint64)
 rx.demod_device(x, bits, valid)
 torch.cuda.synchronize()
 lib.qpsk_debug_stamps(st.ctypes.data, 1)
-lib.qpsk_debug_counts(cnt.ctypes.data, 1)
 rx.demod_device(x, bits, valid)
 torch.cuda.synchronize()
 lib.qpsk_debug_stamps(st.ctypes.data, 1)
-lib.qpsk_debug_counts(cnt.ctypes.data, 1)
 v = [int(t) for t in st]
 bf = back_waves * nf / 2          # back-wave frames
 ff = front_waves * nf             # front-wave frames
@@ -69,6 +63,4 @@ out = {
                                  "argmax (12)": round(v[12] / fc)},
 }
 out["back_steps_cycles"] = round(v[13] / bf / 128)
-if int(cnt[0]):   # QPSK_SPEC fronts: guessed and redone channels
-    out["spec"] = {"guessed": int(cnt[0]), "redone": int(cnt[1]), "redo_frac": round(int(cnt[1]) / int(cnt[0]), 4)}
 print(json.dumps(out, indent=1))

@@ -76,13 +76,6 @@ constexpr int kDec = 296;
 #ifndef QPSK_HUNT_FILTER
 #define QPSK_HUNT_FILTER 1   // 1: bf16 first pass, exact chain only when the argmax is in doubt (qpsk_hunt.h)
 #endif
-#ifndef QPSK_SPEC
-// speculative fronts in the dual-chain kernels (rx_kernel<.., DUAL>): the front
-// of frame n runs ahead of the decision it depends on with a guessed rx_timing
-// and redoes only the channels whose guess the decision contradicts (the front
-// comment in rx_kernel).  0: the fronts wait for the decision (A/B knob)
-#define QPSK_SPEC 0
-#endif
 #ifndef QPSK_DYNPRIO
 // dynamic issue priority of the dual-chain back waves (rx_kernel): they train
 // at the highest priority unless another back wave waits for its fronts.
@@ -140,8 +133,6 @@ struct RxArgs {
                              // bits 8-15: front stagger; bits 16-19: front split
     int* err;                // device error word (kErrStall)
     const float2* heads;     // [nch][F][102] head pre-pass outputs (HP), or null
-    float2* win2;            // QPSK_SPEC dual-chain kernels: the third window buffer (win0 + 2 (win1 - win0))
-    int wrot;                //   (the call's frame n in buffer (wrot + n) mod 3)
 };
 
 // Diagnostic build only (-DQPSK_STAMPS): per-phase cycle sums of the front
@@ -149,14 +140,9 @@ struct RxArgs {
 // is compiled out.
 #ifdef QPSK_STAMPS
 __device__ unsigned long long g_stamps[16];
-__device__ unsigned long long g_counts[4];   // QPSK_SPEC fronts: [0] guessed channels, [1] redone
-// per-wave counts, added to g_counts once at the end (one global atomic per
-// event from every front wave serializes on one L2 line: ~90 per us)
-#define COUNT(i) do { st_cnt[i]++; } while (0)
-#define STAMP_DECL unsigned long long st_acc[16] = {}; unsigned st_cnt[4] = {}; unsigned long long st_t0 = stamp_now();
+#define STAMP_DECL unsigned long long st_acc[16] = {}; unsigned long long st_t0 = stamp_now();
 #define STAMP(i) do { const unsigned long long t_ = stamp_now(); st_acc[i] += t_ - st_t0; st_t0 = t_; } while (0)
-#define STAMP_FLUSH() do { if (lane == 0) { for (int i_ = 0; i_ < 16; i_++) atomicAdd(&g_stamps[i_], st_acc[i_]); \
-                                               for (int i_ = 0; i_ < 4; i_++) atomicAdd(&g_counts[i_], (unsigned long long)st_cnt[i_]); } } while (0)
+#define STAMP_FLUSH() do { if (lane == 0) for (int i_ = 0; i_ < 16; i_++) atomicAdd(&g_stamps[i_], st_acc[i_]); } while (0)
 __device__ __forceinline__ unsigned long long stamp_now() {
     unsigned long long t;
     __builtin_amdgcn_sched_barrier(0);
@@ -166,21 +152,11 @@ __device__ __forceinline__ unsigned long long stamp_now() {
 }
 #else
 #define STAMP_DECL
-#define COUNT(i) do { } while (0)
 #define STAMP(i) do { } while (0)
 #define STAMP_FLUSH() do { } while (0)
 #endif
 
 __device__ __forceinline__ float2* win_of(const RxArgs& a, unsigned g) { return (g & 1u) ? a.win1 : a.win0; }
-// QPSK_SPEC dual-chain kernels: window of the call's frame n (three buffers:
-// the front of frame n writes window n+1 while the back of frame n-1 may still
-// read window n-1; wrot = the context's frame count mod 3, set per call)
-// (the three are one allocation, win1 - win0 apart: a pointer picked among the
-// argument fields by a run-time index put the whole argument block in scratch)
-__device__ __forceinline__ float2* win_spec(const RxArgs& a, int n) {
-    const int s = (a.wrot + n) % 3;
-    return a.win0 + (size_t)s * (size_t)(a.win1 - a.win0);
-}
 __device__ __forceinline__ int* mi_of(const RxArgs& a, unsigned g) { return (g & 1u) ? a.mi1 : a.mi0; }
 __device__ __forceinline__ int* rt_of(const RxArgs& a, unsigned g) { return (g & 1u) ? a.rt1 : a.rt0; }
 
@@ -300,18 +276,9 @@ __device__ __forceinline__ void prefetch_seq(const Src& s, int lane, int (&r)[kP
     (load_item<MODE, I, CG>(s, lane, r[I]), ...);
 }
 
-// the lane index, laundered: per-lane item offsets and signs derived from it are
-// recomputed at each use (a few VALU) instead of being hoisted out of the
-// channel loop as ~20 live registers, which the front (at its 168-VGPR budget)
-// spilled, each reload then waiting for the prefetch in flight
-__device__ __forceinline__ int fresh_lane(int lane) {
-    asm volatile("" : "+v"(lane));
-    return lane;
-}
-
 template <int MODE, bool CG = false>
 __device__ __forceinline__ void prefetch(const Src& s, int lane, int (&r)[kPf<MODE>]) {
-    prefetch_seq<MODE, CG>(s, fresh_lane(lane), r, std::make_integer_sequence<int, kPf<MODE>>{});
+    prefetch_seq<MODE, CG>(s, lane, r, std::make_integer_sequence<int, kPf<MODE>>{});
 }
 
 // src/qpsk.c:139-144 as (-1)^G * P[t] * (x * 2^-14), two samples per item.
@@ -349,7 +316,6 @@ template <int MODE>
 __device__ __forceinline__ void mix(int lane, const int (&r)[kPf<MODE>], unsigned g,
                                     const float2* P, float2* M) {
     constexpr auto kSeq = std::make_integer_sequence<int, kPf<MODE>>{};
-    lane = fresh_lane(lane);
     if (((g - 1u) & 1u) != 0) mix_seq<MODE, true>(lane, r, P, M, kSeq);   // frame g-1 odd
     else mix_seq<MODE, false>(lane, r, P, M, kSeq);
 }
@@ -1426,8 +1392,7 @@ __global__ void __launch_bounds__(64 * (kBackWavesOf<G, FP, MODE, DUAL, W, QUAD>
     const int16_t* in, int16_t* hist, const float2* ptab, const unsigned long long* ks,
     float2* win0, float2* win1, int* mi0, int* mi1, int* rt0, int* rt1, uint8_t* bits,
     uint8_t* valid, int32_t* trace, float2* soft, float4* jobs, unsigned* njobs, int nch, int F,
-    unsigned g0, int roles, const float* fft_tab, unsigned long long jcap, int* err,
-    float2* win2, int wrot) {
+    unsigned g0, int roles, const float* fft_tab, unsigned long long jcap, int* err) {
     static_assert(W == QK_GROUP || (DUAL && G == 1 && W % FP == 0 && W <= QK_GROUP), "group width");
     static_assert(!QUAD || (DUAL && G == 1 && W % 16 == 0), "quad backs: dual chain, one group");
     constexpr int kGroups = G, kFrontPer = FP;
@@ -1440,27 +1405,18 @@ __global__ void __launch_bounds__(64 * (kBackWavesOf<G, FP, MODE, DUAL, W, QUAD>
     const RxArgs a{in, hist, ptab, ks, win0, win1, mi0, mi1, rt0, rt1, bits, valid, trace, soft,
                    jobs, njobs, nch, F, g0, (size_t)jcap, roles, err,
                    // HP (reference mode only): fft_tab carries the head pre-pass outputs
-                   HP ? reinterpret_cast<const float2*>(fft_tab) : nullptr, win2, wrot};
+                   HP ? reinterpret_cast<const float2*>(fft_tab) : nullptr};
     __shared__ __attribute__((aligned(16))) float2 P[QK_FRAME];
     constexpr int DM = MODE & 1;   // decimation semantics; MODE & 2: FFT hunt
     constexpr int kM = Cfg<DM>::kM, kDecBuf = Cfg<DM>::kDecBuf;
     __shared__ __attribute__((aligned(16))) float2 Ms[kFrontWaves][kM];
     __shared__ __attribute__((aligned(16))) float2 decs[kFrontWaves][kDecBuf][kDec];
-    // mi_s: preamble position of frame n in slot n mod 2 (QPSK_SPEC dual-chain:
-    // n mod 3, as the windows); rt_s: rx_timing of frame n in slot n mod 2
-    constexpr bool kSpec = DUAL && QPSK_SPEC;
-    constexpr int kMiSlots = kSpec ? 3 : 2;
-    auto mslot = [](int n) { return kSpec ? n % 3 : n & 1; };
-    __shared__ int mi_s[kGroups][kMiSlots][QK_GROUP], rt_s[kGroups][2][QK_GROUP];
-    // QPSK_SPEC: rx_timing each channel's front of frame n guessed (slot n mod 4),
-    // and per group, parity and block the front waves done with their guesses
-    __shared__ int srt_s[kSpec ? kGroups : 1][4][kSpec ? QK_GROUP : 1];
+    __shared__ int mi_s[kGroups][2][QK_GROUP], rt_s[kGroups][2][QK_GROUP];
     // hunt tables: the MFMA correlator's B, or the FFT hunt's twiddles / Q / permutation
     __shared__ __attribute__((aligned(16))) float BT[(MODE & 2) ? kFftHT : kHuntTab];
     // DUAL progress counters, per group, frame parity and channel block (one
     // block per back wave of a chain)
     __shared__ int bseq[kGroups][2][kChainWaves], fcnt[kGroups][2][kChainWaves];
-    __shared__ int scnt[kGroups][2][kChainWaves];
     __shared__ int dead_s;                               // DUAL: a wait of this workgroup timed out
     __shared__ int nwait_s;                              // kDyn: back waves waiting for their fronts
     const int lane = threadIdx.x & 63;
@@ -1486,8 +1442,7 @@ __global__ void __launch_bounds__(64 * (kBackWavesOf<G, FP, MODE, DUAL, W, QUAD>
             rt_s[wave][0][lane] = rt_of(a, a.g0)[ch];
         }
     }
-    if (threadIdx.x < 2 * kGroups * kChainWaves)
-        (&bseq[0][0][0])[threadIdx.x] = (&fcnt[0][0][0])[threadIdx.x] = (&scnt[0][0][0])[threadIdx.x] = 0;
+    if (threadIdx.x < 2 * kGroups * kChainWaves) (&bseq[0][0][0])[threadIdx.x] = (&fcnt[0][0][0])[threadIdx.x] = 0;
     if (threadIdx.x == 0) dead_s = nwait_s = 0;
     __syncthreads();
     if constexpr (DUAL) {
@@ -1558,15 +1513,14 @@ __global__ void __launch_bounds__(64 * (kBackWavesOf<G, FP, MODE, DUAL, W, QUAD>
                     }
                 }
                 STAMP(14);
-                const int mi = mi_s[gi][mslot(n)][idx];
+                const int mi = mi_s[gi][p][idx];
                 auto get_rt = [&] {   // rx_timing of frame n = the decision of frame n-1
                     STAMP(13);
                     if (n > 0) spin_wait(&bseq[gi][p ^ 1][b], (n - 1) / 2 + 1, a.err, &dead_s);
                     STAMP(15);
                     return rt_s[gi][p][idx];
                 };
-                const float2* wn = (kSpec ? win_spec(a, n) : win_of(a, a.g0 + (unsigned)n)) +
-                                   (size_t)(live ? ch : 0) * kWinStride;
+                const float2* wn = win_of(a, a.g0 + (unsigned)n) + (size_t)(live ? ch : 0) * kWinStride;
                 int* rtn = own ? &rt_s[gi][p ^ 1][idx] : nullptr;
                 if constexpr (QUAD)
                     back_frame_quad(a, live ? ch : 0, live, n, mi, get_rt, wn, rtn, poll);
@@ -1651,113 +1605,7 @@ __global__ void __launch_bounds__(64 * (kBackWavesOf<G, FP, MODE, DUAL, W, QUAD>
             STAMP(5);                                                                                          \
         }                                                                                                      \
     } while (0)
-            if constexpr (kSpec) {
-                // Speculative fronts.  rx_timing of frame n is rt_n = valid_{n-1} ?
-                // mi_{n-1} + 128 : rt_{n-1} (src/qpsk.c:196-219); the front of frame n
-                // (window n+1, mi_{n+1}) needs rt_n, i.e. the decision of frame n-1,
-                // which ends a training of the other chain.  Instead of waiting for
-                // it, a block's front waves run the front of frame n right after the
-                // decision of frame n-2 with the guess rt_{n-1} (srt_s), and when the
-                // decision of frame n-1 comes they redo only the channels whose guess
-                // it contradicts (a valid frame n-1 with a new position: ~35% of the
-                // noiseless bench's channel-frames, fewer with noise), the r-th such
-                // channel of the block on front wave r mod FP.  A guessed window is
-                // kept only when its guess equals rt_n, so every output is the one
-                // rt_n gives.  Per block a wave does: redo of frame n-1, then the
-                // guesses of frame n.  Buffers: the guesses of frame n overwrite
-                // window slot (n+1) mod 3 and mi slot (n+1) mod 3 after the decision
-                // of frame n-2 (their readers, the back of frame n-2, are done); a
-                // redo overwrites a guessed window only after every front wave of
-                // the block has finished its guesses (scnt).
-                int pch = blive(0) > 0 ? bch0(0) : -1, pn = 0;   // what pf holds
-                // CG: every frame this call touches is >= 2 (prefetch<.., true>: one
-                // wave-uniform base; iterations n <= 2 of the loop below also touch
-                // frame 1 and run as a separate copy, as the quad kernels' peel above)
-                auto fetch = [&](auto cg, int ch, int n) {
-                    prefetch<DM, QUAD && decltype(cg)::value>(srcs(a, ch, n), lane, pf);
-                };
-                // one channel of the front of frame n with rx_timing rt; then the
-                // prefetch of (nxch, nxn) if known (nxch >= 0)
-                auto chan = [&](auto cg, int ch, int idx, int n, int rt, int nxch, int nxn) {
-                    if (ch != pch || n != pn) fetch(cg, ch, n);
-                    float2* dcur = decs[f][k % kDecBuf];
-                    k++;
-                    mix<DM>(lane, pf, a.g0 + (unsigned)n, P, M);
-                    STAMP(0);
-                    pch = nxch;
-                    pn = nxn;
-                    if (nxch >= 0) fetch(cg, nxch, nxn);
-                    wave_lds_sync();
-                    STAMP(1);
-                    const int mi = front_channel<MODE, HP>(lane, rt, M, dcur, BT,
-                                                           a.heads + ((size_t)ch * a.F + n) * kHeadOut FACC_ARG);
-                    if (lane == 0) mi_s[gi][mslot(n + 1)][idx] = mi;
-                    STAMP(6);
-                    store_window(lane, mi, dcur, win_spec(a, n + 1) + (size_t)ch * kWinStride);
-                    wave_lds_sync();
-                    STAMP(4);
-                };
-                const int gch0 = (grp0 + gi) * W;   // the group's first channel
-                auto iter = [&](auto cg, int n) {
-                    const int p = n & 1, m = n - 1, q = m & 1;
-                    for (int bb = 0; bb < kChainWaves; bb++) {
-                        const int c0 = bch0(bb), i0 = kBlkCh * bb + cbeg;
-                        const bool fidle = (a.roles & kFrontIdle) != 0;   // profiling only
-                        // this wave's work on block bb: the redo channels of frame m = n-1,
-                        // then (signal) the guesses of frame n; one call site of the
-                        // channel code (two would double the front's code and spill)
-                        const int ns = (n < a.F && !(fidle && n >= 2)) ? blive(bb) : 0;
-                        unsigned long long mm = 0;
-                        bool pend = n >= 1;   // fcnt of frame m still to signal
-                        if (pend) {
-                            if (m > 0) spin_wait(&bseq[gi][q ^ 1][bb], (m - 1) / 2 + 1, a.err, &dead_s);
-                            spin_wait(&scnt[gi][q][bb], kFrontPer * (m / 2 + 1), a.err, &dead_s);
-                            STAMP(7);
-                            const int bi = kBlkCh * bb + lane;
-                            const bool mis = !(fidle && m >= 2) && lane < kBlkCh && gch0 + bi < a.nch &&
-                                             srt_s[gi][m & 3][bi] != rt_s[gi][q][bi];
-                            mm = __ballot(mis);
-                            for (int j = 0; j < fl && mm; j++) mm &= mm - 1ull;   // every FP-th, from the fl-th
-                        }
-                        int c = 0;
-                        for (;;) {
-                            if (pend && !mm) {
-                                signal_add(&fcnt[gi][q][bb], 1, lane);
-                                STAMP(5);
-                                pend = false;
-                            }
-                            if (!mm && c >= ns) break;
-                            int idx, fr, rt, nxch = -1, nxn = n;
-                            if (mm) {   // redo: rt_m
-                                idx = kBlkCh * bb + __ffsll((long long)mm) - 1;
-                                unsigned long long nx = mm & (mm - 1ull);
-                                for (int j = 1; j < kFrontPer && nx; j++) nx &= nx - 1ull;
-                                if (nx) { nxch = gch0 + kBlkCh * bb + __ffsll((long long)nx) - 1; nxn = m; }
-                                else if (ns > 0) nxch = c0;
-                                fr = m;
-                                rt = rt_s[gi][q][idx];
-                                mm = nx;
-                                COUNT(1);
-                            } else {    // guess: rt_{n-1} (n = 0: rt_0 itself)
-                                idx = i0 + c;
-                                fr = n;
-                                rt = rt_s[gi][n == 0 ? 0 : p ^ 1][idx];
-                                if (lane == 0) srt_s[gi][n & 3][idx] = rt;
-                                COUNT(0);
-                                if (c + 1 < ns) nxch = c0 + c + 1;
-                                else
-                                    for (int nb = bb + 1; nb < kChainWaves; nb++)
-                                        if (blive(nb) > 0) { nxch = bch0(nb); break; }
-                                c++;
-                            }
-                            chan(cg, gch0 + idx, idx, fr, rt, nxch, nxn);
-                        }
-                        if (n < a.F) signal_add(&scnt[gi][p][bb], 1, lane);
-                    }
-                };
-                for (int n = 0; n <= a.F && n < 3; n++) iter(std::false_type{}, n);
-                for (int n = 3; n <= a.F; n++) iter(std::true_type{}, n);
-            } else if constexpr (QUAD) {
+            if constexpr (QUAD) {
                 auto frame_iter = [&](auto cg, int n) {
                     constexpr bool CG = decltype(cg)::value;
                     QPSK_DUAL_FRONT_FRAME(CG);
@@ -1780,7 +1628,7 @@ __global__ void __launch_bounds__(64 * (kBackWavesOf<G, FP, MODE, DUAL, W, QUAD>
             const int ch = (grp0 + gi) * W + idx;
             if (sub < kBlkCh && ch < a.nch && (!QUAD || (lane & 3) == 0)) {
                 const unsigned ge = a.g0 + (unsigned)a.F;
-                mi_of(a, ge)[ch] = mi_s[gi][mslot(a.F)][idx];
+                mi_of(a, ge)[ch] = mi_s[gi][a.F & 1][idx];
                 rt_of(a, ge)[ch] = rt_s[gi][a.F & 1][idx];
             }
         }
@@ -1899,7 +1747,7 @@ struct qpsk_ctx {
     float2* d_ptab = nullptr;
     unsigned long long* d_ks = nullptr;
     int16_t* d_hist = nullptr;
-    float2* d_win[3] = {nullptr, nullptr, nullptr};   // [2]: QPSK_SPEC dual-chain kernels
+    float2* d_win[2] = {nullptr, nullptr};
     int* d_mi[2] = {nullptr, nullptr};
     int* d_rt[2] = {nullptr, nullptr};
     // data-symbol jobs of valid frames (rx_kernel -> rx_data_kernel)
@@ -1989,10 +1837,8 @@ static int ctx_alloc(qpsk_ctx* c) {
     HCHECK(hipMalloc(&c->d_njobs, sizeof(unsigned) * 2));
     HCHECK(hipMalloc(&c->d_err, 2 * sizeof(int)));
     HCHECK(hipEventCreateWithFlags(&c->done, hipEventDisableTiming));
-    // the three window buffers in one allocation (win_spec() steps by d_win[1] - d_win[0])
-    HCHECK(hipMalloc(&c->d_win[0], 3 * sizeof(float2) * nslot(c) * kWinStride));
-    for (int p = 1; p < 3; p++) c->d_win[p] = c->d_win[0] + (size_t)p * nslot(c) * kWinStride;
     for (int p = 0; p < 2; p++) {
+        HCHECK(hipMalloc(&c->d_win[p], sizeof(float2) * nslot(c) * kWinStride));
         HCHECK(hipMalloc(&c->d_mi[p], sizeof(int) * nslot(c)));
         HCHECK(hipMalloc(&c->d_rt[p], sizeof(int) * nslot(c)));
     }
@@ -2006,8 +1852,10 @@ extern "C" int qpsk_rx_reset(qpsk_ctx* c) {
     HCHECK(hipMemsetAsync(c->d_hist, 0, sizeof(int16_t) * ns * 2 * QK_FRAME, c->stream));
     HCHECK(hipMemsetAsync(c->d_njobs, 0, sizeof(unsigned) * 2, c->stream));
     HCHECK(hipMemsetAsync(c->d_err, 0, 2 * sizeof(int), c->stream));
-    for (int p = 0; p < 3; p++) HCHECK(hipMemsetAsync(c->d_win[p], 0, sizeof(float2) * ns * kWinStride, c->stream));
-    for (int p = 0; p < 2; p++) HCHECK(hipMemsetAsync(c->d_mi[p], 0, sizeof(int) * ns, c->stream));
+    for (int p = 0; p < 2; p++) {
+        HCHECK(hipMemsetAsync(c->d_win[p], 0, sizeof(float2) * ns * kWinStride, c->stream));
+        HCHECK(hipMemsetAsync(c->d_mi[p], 0, sizeof(int) * ns, c->stream));
+    }
     int* rt0 = (int*)malloc(sizeof(int) * ns);
     if (!rt0) return QPSK_ENOMEM;
     for (size_t i = 0; i < ns; i++) rt0[i] = QK_RT0;
@@ -2038,8 +1886,8 @@ static void ctx_free(qpsk_ctx* c) {
     (void)hipFree(c->d_hist);
     (void)hipFree(c->d_fft);
     (void)hipFree(c->d_heads);
-    (void)hipFree(c->d_win[0]);
     for (int p = 0; p < 2; p++) {
+        (void)hipFree(c->d_win[p]);
         (void)hipFree(c->d_mi[p]);
         (void)hipFree(c->d_rt[p]);
     }
@@ -2259,7 +2107,7 @@ int qpsk_rx_launch(qpsk_ctx* c, const int16_t* d_in, int F, uint8_t* d_bits, uin
                        c->d_jobs, c->d_njobs + parity, c->nch, F,                               \
                        (unsigned)(c->frames & 0xffffffffu), sh.roles,                          \
                        HH ? reinterpret_cast<const float*>(c->d_heads) : c->d_fft,             \
-                       (unsigned long long)c->jobs_cap, d_err, c->d_win[2], (int)(c->frames % 3u))
+                       (unsigned long long)c->jobs_cap, d_err)
 #define QPSK_LAUNCH_SHAPES(MM, HH)                                                             \
     do {                                                                                       \
         switch (sh.kind) {                                                                     \
@@ -2460,15 +2308,6 @@ extern "C" int qpsk_rx_batch(qpsk_ctx* c, const int16_t* in, int F, uint8_t* bit
 }
 
 #ifdef QPSK_STAMPS
-extern "C" int qpsk_debug_counts(unsigned long long* out4, int reset) {
-    if (hipMemcpyFromSymbol(out4, HIP_SYMBOL(g_counts), sizeof(unsigned long long) * 4) != hipSuccess)
-        return -1;
-    if (reset) {
-        unsigned long long z[4] = {0};
-        if (hipMemcpyToSymbol(HIP_SYMBOL(g_counts), z, sizeof z) != hipSuccess) return -1;
-    }
-    return 0;
-}
 extern "C" int qpsk_debug_stamps(unsigned long long* out16, int reset) {
     if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 16) != hipSuccess)
         return -1;
