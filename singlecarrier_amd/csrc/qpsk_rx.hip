@@ -70,6 +70,9 @@ constexpr int kDec = 296;
 #ifndef QPSK_FIR_SB
 #define QPSK_FIR_SB 0   // 1: scheduling barrier after each FIR batch (register pressure A/B knob)
 #endif
+#ifndef QPSK_FRESH
+#define QPSK_FRESH 0   // 1: recompute the prefetch/mixer per-lane constants at each use (register A/B knob)
+#endif
 #ifndef QPSK_HUNT_MFMA
 #define QPSK_HUNT_MFMA 1   // 1: hunt on the matrix cores; 0: packed VALU chains (A/B knob)
 #endif
@@ -276,9 +279,17 @@ __device__ __forceinline__ void prefetch_seq(const Src& s, int lane, int (&r)[kP
     (load_item<MODE, I, CG>(s, lane, r[I]), ...);
 }
 
+// the lane index, laundered: per-lane item offsets and signs derived from it are
+// recomputed at each use (a few VALU) instead of being hoisted out of the
+// channel loop as live registers
+__device__ __forceinline__ int fresh_lane(int lane) {
+    asm volatile("" : "+v"(lane));
+    return lane;
+}
+
 template <int MODE, bool CG = false>
 __device__ __forceinline__ void prefetch(const Src& s, int lane, int (&r)[kPf<MODE>]) {
-    prefetch_seq<MODE, CG>(s, lane, r, std::make_integer_sequence<int, kPf<MODE>>{});
+    prefetch_seq<MODE, CG>(s, QPSK_FRESH ? fresh_lane(lane) : lane, r, std::make_integer_sequence<int, kPf<MODE>>{});
 }
 
 // src/qpsk.c:139-144 as (-1)^G * P[t] * (x * 2^-14), two samples per item.
@@ -316,6 +327,7 @@ template <int MODE>
 __device__ __forceinline__ void mix(int lane, const int (&r)[kPf<MODE>], unsigned g,
                                     const float2* P, float2* M) {
     constexpr auto kSeq = std::make_integer_sequence<int, kPf<MODE>>{};
+    if (QPSK_FRESH) lane = fresh_lane(lane);
     if (((g - 1u) & 1u) != 0) mix_seq<MODE, true>(lane, r, P, M, kSeq);   // frame g-1 odd
     else mix_seq<MODE, false>(lane, r, P, M, kSeq);
 }
@@ -1385,10 +1397,15 @@ __global__ void __launch_bounds__(256) rx_data_kernel(const float4* jobs, unsign
 template <int G, int FP, int MODE, bool DUAL, int W, bool QUAD>
 constexpr int kBackWavesOf = DUAL ? 2 * G * (QUAD ? W / 16 : 1) : G;
 
+// waves per SIMD = ceil(waves / 4): 3 (<= 168 VGPRs) for the 12-wave shapes, 2 for 1x4
+template <int G, int FP, int MODE, bool DUAL, int W, bool QUAD>
+constexpr int kWavesOf = kBackWavesOf<G, FP, MODE, DUAL, W, QUAD> + G * FP;
+
 //
 // HP: the fronts take F_{n+1} from the head pre-pass (head_kernel, QPSK_HEADPASS).
 template <int G, int FP, int MODE, bool DUAL, int W = QK_GROUP, bool QUAD = false, bool HP = false>
-__global__ void __launch_bounds__(64 * (kBackWavesOf<G, FP, MODE, DUAL, W, QUAD> + G * FP), 3) QPSK_RX_ATTR rx_kernel(
+__global__ void __launch_bounds__((64 * kWavesOf<G, FP, MODE, DUAL, W, QUAD>),
+                                  ((kWavesOf<G, FP, MODE, DUAL, W, QUAD> + 3) / 4)) QPSK_RX_ATTR rx_kernel(
     const int16_t* in, int16_t* hist, const float2* ptab, const unsigned long long* ks,
     float2* win0, float2* win1, int* mi0, int* mi1, int* rt0, int* rt1, uint8_t* bits,
     uint8_t* valid, int32_t* trace, float2* soft, float4* jobs, unsigned* njobs, int nch, int F,
@@ -1728,7 +1745,7 @@ float bits2f(uint32_t u) {
 
 // rx_kernel instantiations (pick_shape below)
 struct Shape {
-    enum Kind { k4x2, k2x4d, k1x8d16, k1x8d32, k1x8d64, k1x8q16, k1x8q32 };
+    enum Kind { k4x2, k2x4d, k1x8d16, k1x8d32, k1x8d64, k1x8q16, k1x8q32, k1x4q16, k1x4q32 };
     int kind;
     int roles;
 };
@@ -1778,6 +1795,7 @@ struct qpsk_ctx {
     int shape = -1;             // Shape::Kind forced by QPSK_SHAPE (A/B runs); -1: by batch size
     int width = 0;              // dual-chain group width forced by QPSK_WIDTH; 0: by batch size
     int quad = -1;              // quad-per-channel backs forced on/off by QPSK_QUAD; -1: by width
+    int fronts = 0;             // front waves of the quad shapes forced by QPSK_FRONTS (4 | 8); 0: by width
     int prio = -1;              // issue priority forced by QPSK_PRIO (0 none, 1 front, 2 back)
     bool headpass = false;      // QPSK_HEADPASS: the FIR-head pre-pass (reference mode only)
     float2* d_heads = nullptr;  // its outputs, [nch][F][102] for the largest call
@@ -1963,6 +1981,7 @@ extern "C" qpsk_ctx* qpsk_rx_create_mode(int device, int nch, int mode, int* err
         c->width = (v == 16 || v == 32 || v == 64) ? v : 0;
     }
     if (const char* qv = getenv("QPSK_QUAD")) c->quad = atoi(qv) != 0;
+    if (const char* fv = getenv("QPSK_FRONTS")) c->fronts = atoi(fv) == 4 ? 4 : atoi(fv) == 8 ? 8 : 0;
     if (const char* hv = getenv("QPSK_HEADPASS")) c->headpass = atoi(hv) != 0 && mode == QPSK_MODE_REFERENCE;
     if (const char* pv = getenv("QPSK_PRIO"))
         c->prio = !strcmp(pv, "none") ? 0 : !strcmp(pv, "front") ? 1 : !strcmp(pv, "back") ? 2 : -1;
@@ -2035,7 +2054,8 @@ static Shape pick_shape(const qpsk_ctx* c) {
         // lane-per-channel back stays there (profiles/r02_quad_ab.txt)
         const bool quad = W <= 32 && (c->quad >= 0 ? c->quad != 0 : true);
         if (quad) {
-            sh.kind = W == 16 ? Shape::k1x8q16 : Shape::k1x8q32;
+            const bool f4 = c->fronts == 4;
+            sh.kind = W == 16 ? (f4 ? Shape::k1x4q16 : Shape::k1x8q16) : (f4 ? Shape::k1x4q32 : Shape::k1x8q32);
         } else {
             sh.kind = W == 16 ? Shape::k1x8d16 : W == 32 ? Shape::k1x8d32 : Shape::k1x8d64;
             if (W == 64) sh.roles = (sh.roles & ~((3 << 4) | (15 << 16))) | (2 << 4) | (2 << 16);
@@ -2117,6 +2137,8 @@ int qpsk_rx_launch(qpsk_ctx* c, const int16_t* d_in, int F, uint8_t* d_bits, uin
             case Shape::k1x8d64: QPSK_LAUNCH(1, 8, MM, true, 64, false, HH); break;            \
             case Shape::k1x8q16: QPSK_LAUNCH(1, 8, MM, true, 16, true, HH); break;             \
             case Shape::k1x8q32: QPSK_LAUNCH(1, 8, MM, true, 32, true, HH); break;             \
+            case Shape::k1x4q16: QPSK_LAUNCH(1, 4, MM, true, 16, true, HH); break;             \
+            case Shape::k1x4q32: QPSK_LAUNCH(1, 4, MM, true, 32, true, HH); break;             \
             default: QPSK_LAUNCH(4, 2, MM, false, 64, false, HH); break;                       \
         }                                                                                      \
     } while (0)
