@@ -1745,7 +1745,7 @@ float bits2f(uint32_t u) {
 
 // rx_kernel instantiations (pick_shape below)
 struct Shape {
-    enum Kind { k4x2, k2x4d, k1x8d16, k1x8d32, k1x8d64, k1x8q16, k1x8q32, k1x4q16, k1x4q32 };
+    enum Kind { k4x2, k2x4d, k1x8d16, k1x8d32, k1x8d64, k1x8q16, k1x8q32, k1x4q16, k1x4q32, k1x4q64 };
     int kind;
     int roles;
 };
@@ -2052,10 +2052,13 @@ static Shape pick_shape(const qpsk_ctx* c) {
         // quad backs need W / 16 back waves per chain: at W = 64 that is 16
         // waves per workgroup, whose 128-VGPR budget spills the front; the
         // lane-per-channel back stays there (profiles/r02_quad_ab.txt)
-        const bool quad = W <= 32 && (c->quad >= 0 ? c->quad != 0 : true);
+        // (1x4 -- one front per SIMD, QPSK_FRONTS=4 -- leaves room for the 8 quad back
+        // waves of W = 64: 12 waves)
+        const bool f4 = c->fronts == 4;
+        const bool quad = (W <= 32 || f4) && (c->quad >= 0 ? c->quad != 0 : W <= 32);
         if (quad) {
-            const bool f4 = c->fronts == 4;
-            sh.kind = W == 16 ? (f4 ? Shape::k1x4q16 : Shape::k1x8q16) : (f4 ? Shape::k1x4q32 : Shape::k1x8q32);
+            sh.kind = W == 16 ? (f4 ? Shape::k1x4q16 : Shape::k1x8q16)
+                    : W == 32 ? (f4 ? Shape::k1x4q32 : Shape::k1x8q32) : Shape::k1x4q64;
         } else {
             sh.kind = W == 16 ? Shape::k1x8d16 : W == 32 ? Shape::k1x8d32 : Shape::k1x8d64;
             if (W == 64) sh.roles = (sh.roles & ~((3 << 4) | (15 << 16))) | (2 << 4) | (2 << 16);
@@ -2139,6 +2142,7 @@ int qpsk_rx_launch(qpsk_ctx* c, const int16_t* d_in, int F, uint8_t* d_bits, uin
             case Shape::k1x8q32: QPSK_LAUNCH(1, 8, MM, true, 32, true, HH); break;             \
             case Shape::k1x4q16: QPSK_LAUNCH(1, 4, MM, true, 16, true, HH); break;             \
             case Shape::k1x4q32: QPSK_LAUNCH(1, 4, MM, true, 32, true, HH); break;             \
+            case Shape::k1x4q64: QPSK_LAUNCH(1, 4, MM, true, 64, true, HH); break;             \
             default: QPSK_LAUNCH(4, 2, MM, false, 64, false, HH); break;                       \
         }                                                                                      \
     } while (0)
