@@ -23,7 +23,8 @@ import singlecarrier_amd as sc  # noqa: E402
 
 nch = int(sys.argv[1])
 nf = int(sys.argv[2]) if len(sys.argv) > 2 else 32
-sc.LIB_PATH = os.path.join(ROOT, "singlecarrier_amd", "csrc", "build", "libqpsk_hip_stamps.so")
+sc.LIB_PATH = os.environ.get("QPSK_STAMPS_LIB") or os.path.join(ROOT, "singlecarrier_amd", "csrc", "build",
+                                                                 "libqpsk_hip_stamps.so")
 lib = sc.lib()
 lib.qpsk_debug_stamps.argtypes = [C.c_void_p, C.c_int]
 import torch  # noqa: E402
@@ -33,7 +34,7 @@ W = int(os.environ.get("QPSK_WIDTH", "0")) or (16 if nch <= 16 * ncu else 32 if 
 quad = int(os.environ.get("QPSK_QUAD", "1" if W <= 32 else "0"))
 nwg = (nch + W - 1) // W
 back_waves = nwg * 2 * (W // (16 * quad) if quad else 1)
-front_waves = nwg * 8
+front_waves = nwg * (4 if os.environ.get("QPSK_FRONTS") == "4" and quad else 8)
 x = torch.from_numpy(sc.synth(3, nch, nf)).cuda()
 bits = torch.empty((nch, nf, 62), dtype=torch.uint8, device="cuda")
 valid = torch.empty((nch, nf), dtype=torch.uint8, device="cuda")
