@@ -31,7 +31,7 @@ import torch  # noqa: E402
 
 ncu = torch.cuda.get_device_properties(0).multi_processor_count
 W = int(os.environ.get("QPSK_WIDTH", "0")) or (16 if nch <= 16 * ncu else 32 if nch <= 32 * ncu else 64)
-quad = int(os.environ.get("QPSK_QUAD", "1" if W <= 32 else "0"))
+quad = int(os.environ.get("QPSK_QUAD", "1" if (W <= 32 or os.environ.get("QPSK_FRONTS") == "4") else "0"))
 nwg = (nch + W - 1) // W
 back_waves = nwg * 2 * (W // (16 * quad) if quad else 1)
 front_waves = nwg * (4 if os.environ.get("QPSK_FRONTS") == "4" and quad else 8)

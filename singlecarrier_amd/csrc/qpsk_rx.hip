@@ -2055,7 +2055,7 @@ static Shape pick_shape(const qpsk_ctx* c) {
         // (1x4 -- one front per SIMD, QPSK_FRONTS=4 -- leaves room for the 8 quad back
         // waves of W = 64: 12 waves)
         const bool f4 = c->fronts == 4;
-        const bool quad = (W <= 32 || f4) && (c->quad >= 0 ? c->quad != 0 : W <= 32);
+        const bool quad = (W <= 32 || f4) && (c->quad >= 0 ? c->quad != 0 : true);
         if (quad) {
             sh.kind = W == 16 ? (f4 ? Shape::k1x4q16 : Shape::k1x8q16)
                     : W == 32 ? (f4 ? Shape::k1x4q32 : Shape::k1x8q32) : Shape::k1x4q64;

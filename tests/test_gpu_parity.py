@@ -443,3 +443,24 @@ def test_quad_backs_across_call_splits(nch):
         a = b
     out = {k: np.concatenate([p[k] for p in parts], axis=1) for k in ("bits", "valid", "trace", "soft")}
     _assert_same(out, bits, valid, tr)
+
+
+@pytest.mark.parametrize("width", ["16", "32", "64"])
+def test_one_front_per_simd_shapes(width, monkeypatch):
+    """QPSK_FRONTS=4 (A/B knob, DESIGN.md "Measured and not kept"): the 1x4
+    quad shapes -- 4 front waves, one per SIMD; at W = 64 the 8 quad back
+    waves (4 blocks per chain) that only this shape leaves room for -- on a
+    ragged batch, and across call splits at W = 32."""
+    monkeypatch.setenv("QPSK_FRONTS", "4")
+    monkeypatch.setenv("QPSK_WIDTH", width)
+    x = oracle.synth(71, 333, 15, 4.0)
+    _vs_oracle(x)
+    if width == "32":
+        bits, valid, tr = oracle.cpu_rx(x, trace=True)
+        rx = sc.Receiver(333)
+        parts, a = [], 0
+        for b in (1, 2, 6, 15):
+            parts.append(rx.demod(np.ascontiguousarray(x[:, a:b]), trace=True, soft=True))
+            a = b
+        out = {k: np.concatenate([p[k] for p in parts], axis=1) for k in ("bits", "valid", "trace", "soft")}
+        _assert_same(out, bits, valid, tr)
