@@ -426,18 +426,21 @@ __device__ __forceinline__ int fft_hunt(int lane, float2* M, const float2* dec, 
 // RRC (src/fir.c:36-42), outputs accumulated in tap order.  Decimated outputs
 // D[o] = fir_out[5o + rt] (model A): lane l makes o = 3l..3l+2
 // from the 59 samples M[15l + rt + s], read in batches.
+// FB samples per LDS batch; SB: a scheduling barrier after each batch (the
+// 4x3 front: bounds the samples in flight at its 128-VGPR budget)
+template <int FB = QPSK_FB, bool SB = QPSK_FIR_SB != 0>
 __device__ __forceinline__ void fir_dec(int lane, int rt, const float2* M, float2* dec) {
     if (lane < 63) {
         const float2* b = M + 15 * lane + rt;
         f2 y[3] = {{0.0f, 0.0f}, {0.0f, 0.0f}, {0.0f, 0.0f}};
 #pragma unroll
-        for (int s0 = 0; s0 < 59; s0 += QPSK_FB) {
-            f2 v[QPSK_FB];
+        for (int s0 = 0; s0 < 59; s0 += FB) {
+            f2 v[FB];
 #pragma unroll
-            for (int j = 0; j < QPSK_FB; j++)
+            for (int j = 0; j < FB; j++)
                 if (s0 + j < 59) v[j] = ld2nt(b + s0 + j);
 #pragma unroll
-            for (int j = 0; j < QPSK_FB; j++) {
+            for (int j = 0; j < FB; j++) {
                 const int s = s0 + j;
 #pragma unroll
                 for (int m = 0; m < 3; m++) {
@@ -445,9 +448,7 @@ __device__ __forceinline__ void fir_dec(int lane, int rt, const float2* M, float
                     if (s < 59 && k >= 0 && k < QK_NTAPS) y[m] = y[m] + v[j] * QK_RRC[k];
                 }
             }
-#if QPSK_FIR_SB
-            __builtin_amdgcn_sched_barrier(0);   // keep the next batch's loads behind this one
-#endif
+            if (SB) __builtin_amdgcn_sched_barrier(0);   // keep the next batch's loads behind this one
         }
 #pragma unroll
         for (int m = 0; m < 3; m++)
@@ -1733,6 +1734,211 @@ __global__ void __launch_bounds__((64 * kWavesOf<G, FP, MODE, DUAL, W, QUAD>),
     }
 }
 
+// ---------------------------------------------------------------- 4x3 (C3 at 4 waves per SIMD)
+// rx43_kernel: 4 groups x (1 lane back + 3 fronts) = 16 waves, 4 per SIMD
+// (<= 128 VGPRs), one workgroup per CU; reference mode only (QPSK_SHAPE=4x3).
+// The 4x2 pipeline (one __syncthreads() per frame) with two changes that let
+// twelve fronts fit:
+// - the roles are separate functions (noinline): each is register-allocated
+//   on its own (compiled together in one kernel body both spill at 128 VGPRs,
+//   DESIGN.md round-4 item 2); they read the kernel argument block through the
+//   kernarg pointer (wave-uniform, scalar loads) and the LDS state as
+//   namespace-scope arrays;
+// - compact front input: the decimated FIR reads M[rt .. rt + 983] only, so a
+//   front mixes [rt0, rt0 + 986) (rt0 = rt & ~1) and the 152-sample head: 569
+//   two-sample items instead of 696, 9.1 KB of LDS per front; one dec buffer
+//   (the window is stored before the next channel's FIR).  The prefetch of a
+//   channel needs its rx_timing: the next channel of the frame is fetched after
+//   the current one's FIR, the frame's first channel after the frame barrier.
+#ifndef QPSK_FB43
+#define QPSK_FB43 8   // FIR samples per LDS batch in the 4x3 front (A/B knob)
+#endif
+namespace r43 {
+constexpr int kG = 4, kFP = 3, kFW = kG * kFP, kWaves = kG + kFW;
+constexpr int kMc = 1138;                    // float2: D part [rt0, rt0 + 986) ++ head [1240, 1392)
+constexpr int kHc = 986;                     // the head part's offset in Mc
+constexpr int kItems = kMc / 2;              // 569 two-sample items
+constexpr int kPfC = (kItems + 63) / 64;     // 9 per lane
+__shared__ __attribute__((aligned(16))) float2 sP[QK_FRAME];
+__shared__ __attribute__((aligned(16))) float2 sM[kFW][kMc];
+__shared__ __attribute__((aligned(16))) float2 sDec[kFW][kDec];
+__shared__ int sMi[kG][2][QK_GROUP], sRt[kG][2][QK_GROUP];
+__shared__ __attribute__((aligned(16))) float sBT[kHuntTab];
+
+// the launch's argument block, copied to LDS by the kernel (a called function
+// receives no kernarg segment pointer), read back wave-uniform (SGPRs)
+__shared__ RxArgs sArgs;
+static_assert(sizeof(RxArgs) % 4 == 0, "RxArgs as dwords");
+__device__ __forceinline__ RxArgs kargs() {
+    RxArgs r;
+    int* d = reinterpret_cast<int*>(&r);
+    const int* s = reinterpret_cast<const int*>(&sArgs);
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(RxArgs) / 4); i++) d[i] = __builtin_amdgcn_readfirstlane(s[i]);
+    return r;
+}
+
+// item d = lane + 64 i of the compact input: two samples at M index k (the
+// 4x2 front's M: k < 48 x_{n-2}[1832 + k], k < 1240 x_{n-1}[k - 48], k < 1288
+// x_{n-1}[1832 + k - 1240], else x_n[k - 1288]); returns the frame (0: n-2,
+// 1: n-1, 2: n) or -1, and the sample index t
+template <int i>
+__device__ __forceinline__ int item(int lane, int rt0, int& t) {
+    const int d = lane + 64 * i;
+    int k;
+    if (i < 7) k = rt0 + 2 * d;
+    else if (i == 7) k = d < 493 ? rt0 + 2 * d : 1240 + 2 * (d - 493);
+    else {
+        if (d >= kItems) { t = 0; return -1; }
+        k = 1240 + 2 * (d - 493);
+    }
+    if (i == 0 && k < 48) { t = 1832 + k; return 0; }   // rt < 48 only (rx_timing 3 before a first valid frame)
+    if (i < 7 || (i == 7 && d < 493)) { t = k - 48; return 1; }
+    if (k < 1288) { t = 1832 + (k - 1240); return 1; }
+    t = k - 1288;
+    return 2;
+}
+
+template <int i>
+__device__ __forceinline__ void load_item(const Src& s, int lane, int rt0, int& r) {
+    int t;
+    const int f = item<i>(lane, rt0, t);
+    if (f >= 0) r = *reinterpret_cast<const int*>((f == 0 ? s.xm2 : f == 1 ? s.xm1 : s.x0) + t);
+}
+template <int... I>
+__device__ __forceinline__ void prefetch_seq(const Src& s, int lane, int rt0, int (&r)[kPfC],
+                                             std::integer_sequence<int, I...>) {
+    (load_item<I>(s, lane, rt0, r[I]), ...);
+}
+__device__ __forceinline__ void prefetch(const Src& s, int lane, int rt0, int (&r)[kPfC]) {
+    prefetch_seq(s, fresh_lane(lane), rt0, r, std::make_integer_sequence<int, kPfC>{});
+}
+
+// mix_item of the 4x2 front on the compact item map: (-1)^G P[t] x 2^-14,
+// frame g-1 negated when NO
+template <int i, bool NO>
+__device__ __forceinline__ void mix_item(int lane, int rt0, int r, float2* M) {
+    int t;
+    const int f = item<i>(lane, rt0, t);
+    if (f < 0) return;
+    const float4 p = *reinterpret_cast<const float4*>(sP + t);
+    const float v0 = (float)(int16_t)(r & 0xffff);
+    const float v1 = (float)(int16_t)(r >> 16);
+    float4 o;
+    if (i >= 1 && i <= 7) {   // every lane's item is from frame g-1
+        o = NO ? make_float4((-p.x) * v0, (-p.y) * v0, (-p.z) * v1, (-p.w) * v1)
+               : make_float4(p.x * v0, p.y * v0, p.z * v1, p.w * v1);
+    } else {
+        const float sg = ((f == 1) == NO) ? -1.0f : 1.0f;   // exact sign flip
+        o = make_float4((sg * p.x) * v0, (sg * p.y) * v0, (sg * p.z) * v1, (sg * p.w) * v1);
+    }
+    *reinterpret_cast<float4*>(M + 2 * (lane + 64 * i)) = o;
+}
+template <bool NO, int... I>
+__device__ __forceinline__ void mix_seq(int lane, int rt0, const int (&r)[kPfC], float2* M,
+                                        std::integer_sequence<int, I...>) {
+    (mix_item<I, NO>(lane, rt0, r[I], M), ...);
+}
+__device__ __forceinline__ void mix(int lane, int rt0, const int (&r)[kPfC], unsigned g, float2* M) {
+    constexpr auto kSeq = std::make_integer_sequence<int, kPfC>{};
+    lane = fresh_lane(lane);
+    if (((g - 1u) & 1u) != 0) mix_seq<true>(lane, rt0, r, M, kSeq);   // frame g-1 odd
+    else mix_seq<false>(lane, rt0, r, M, kSeq);
+}
+
+// the back role (lane = channel): the 4x2 back on this kernel's LDS state
+__device__ __attribute__((noinline)) void back_role() {
+    const RxArgs a = kargs();
+    const int lane = __lane_id();
+    const int gi = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int ch = ((int)blockIdx.x * kG + gi) * QK_GROUP + lane;
+    const bool live = ch < a.nch;
+    const bool any = ((int)blockIdx.x * kG + gi) * QK_GROUP < a.nch;
+    if (((a.roles >> 4) & 3) == 2) __builtin_amdgcn_s_setprio(2);
+    for (int n = 0; n < a.F; n++) {
+        const int p = n & 1;
+        if (any && (a.roles & 1)) {
+            const int rt = sRt[gi][p][lane];
+            back_frame(a, live ? ch : 0, live, n, sMi[gi][p][lane], [=] { return rt; },
+                       win_of(a, a.g0 + (unsigned)n) + (size_t)(live ? ch : 0) * kWinStride,
+                       &sRt[gi][p ^ 1][lane], [] {});
+        } else {
+            sRt[gi][p ^ 1][lane] = sRt[gi][p][lane];
+        }
+        __syncthreads();
+    }
+    if (live) {   // per-channel state after the call's last frame
+        const unsigned ge = a.g0 + (unsigned)a.F;
+        mi_of(a, ge)[ch] = sMi[gi][a.F & 1][lane];
+        rt_of(a, ge)[ch] = sRt[gi][a.F & 1][lane];
+    }
+}
+
+// the front role: channels [cbeg, cbeg + 21 or 22) of its group, one at a time
+__device__ __attribute__((noinline)) void front_role() {
+    const RxArgs a = kargs();
+    const int lane = __lane_id();
+    const int f = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) - kG;
+    const int gi = f / kFP, fl = f % kFP;
+    const int cbeg = 21 * fl, cnt = fl == kFP - 1 ? QK_GROUP - 21 * (kFP - 1) : 21;
+    const int ch0 = ((int)blockIdx.x * kG + gi) * QK_GROUP + cbeg;
+    const int nlive = max(0, min(cnt, a.nch - ch0));
+    float2* M = sM[f];
+    float2* dec = sDec[f];
+    const bool on = (a.roles & 2) != 0 && nlive > 0;
+    if (((a.roles >> 4) & 3) == 1) __builtin_amdgcn_s_setprio(2);
+    int pf[kPfC];
+    for (int n = 0; n < a.F; n++) {
+        const int p = n & 1;
+        const unsigned g = a.g0 + (unsigned)n;
+        float2* wout = win_of(a, g + 1u);
+        if (on) prefetch(srcs(a, ch0, n), lane, sRt[gi][p][cbeg] & ~1, pf);
+        for (int c = 0; on && c < nlive; c++) {
+            const int ch = ch0 + c, idx = cbeg + c;
+            const int rt = sRt[gi][p][idx], rt0 = rt & ~1;
+            mix(lane, rt0, pf, g, M);
+            wave_lds_sync();
+            fir_dec<QPSK_FB43, true>(fresh_lane(lane), rt - rt0, M, dec);
+            fir_head_at(fresh_lane(lane), M + kHc, dec + QK_NDEC);
+            wave_lds_sync();
+            const int mi = hunt<0>(fresh_lane(lane), M, dec, sBT);
+            if (c + 1 < nlive)   // the next channel, after the FIR and hunt: pf is live across neither
+                prefetch(srcs(a, ch + 1, n), lane, sRt[gi][p][idx + 1] & ~1, pf);
+            if (lane == 0) sMi[gi][p ^ 1][idx] = mi;
+            store_window(fresh_lane(lane), mi, dec, wout + (size_t)ch * kWinStride);
+            wave_lds_sync();
+        }
+        __syncthreads();
+    }
+    carry_history<0>(a.in, a.hist, a.F, ch0, nlive, lane);
+}
+}  // namespace r43
+
+__global__ void __launch_bounds__(64 * r43::kWaves, 4) rx43_kernel(const RxArgs args) {
+    using namespace r43;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    constexpr int kBlock = 64 * kWaves;
+    for (int i = threadIdx.x; i < QK_FRAME / 2; i += kBlock)
+        reinterpret_cast<float4*>(sP)[i] = reinterpret_cast<const float4*>(args.ptab)[i];
+#if QPSK_HUNT_FILTER
+    qhunt::bconst_h_lds(threadIdx.x, kBlock, sBT);
+#else
+    qhunt::bconst_lds(threadIdx.x, kBlock, sBT);
+#endif
+    if (wave < kG) {   // per-channel state of the groups at the call's first frame
+        const int ch = ((int)blockIdx.x * kG + wave) * QK_GROUP + lane;
+        if (ch < args.nch) {
+            sMi[wave][0][lane] = mi_of(args, args.g0)[ch];
+            sRt[wave][0][lane] = rt_of(args, args.g0)[ch];
+        }
+    }
+    if (threadIdx.x == 0) sArgs = args;
+    __syncthreads();
+    if (wave < kG) back_role();
+    else front_role();
+}
+
 // ---------------------------------------------------------------- host side
 
 float bits2f(uint32_t u) {
@@ -1745,7 +1951,7 @@ float bits2f(uint32_t u) {
 
 // rx_kernel instantiations (pick_shape below)
 struct Shape {
-    enum Kind { k4x2, k2x4d, k1x8d16, k1x8d32, k1x8d64, k1x8q16, k1x8q32, k1x4q16, k1x4q32, k1x4q64 };
+    enum Kind { k4x2, k2x4d, k1x8d16, k1x8d32, k1x8d64, k1x8q16, k1x8q32, k1x4q16, k1x4q32, k1x4q64, k4x3 };
     int kind;
     int roles;
 };
@@ -1986,7 +2192,8 @@ extern "C" qpsk_ctx* qpsk_rx_create_mode(int device, int nch, int mode, int* err
     if (const char* pv = getenv("QPSK_PRIO"))
         c->prio = !strcmp(pv, "none") ? 0 : !strcmp(pv, "front") ? 1 : !strcmp(pv, "back") ? 2 : -1;
     if (const char* sh = getenv("QPSK_SHAPE")) {
-        c->shape = !strcmp(sh, "4x2") ? Shape::k4x2 : !strcmp(sh, "2x4d") ? Shape::k2x4d
+        c->shape = !strcmp(sh, "4x2") ? Shape::k4x2 : !strcmp(sh, "4x3") ? Shape::k4x3
+                 : !strcmp(sh, "2x4d") ? Shape::k2x4d
                  : !strcmp(sh, "1x8") ? Shape::k1x8d64 : -1;
     }
     int r = herr(hipSetDevice(device));
@@ -2147,7 +2354,18 @@ int qpsk_rx_launch(qpsk_ctx* c, const int16_t* d_in, int F, uint8_t* d_bits, uin
         }                                                                                      \
     } while (0)
 #define QPSK_LAUNCH_MODE(MM) QPSK_LAUNCH_SHAPES(MM, false)
-    if (hp) {   // head pre-pass: every channel-frame's F_{n+1}, then the frame loop
+    if (sh.kind == Shape::k4x3 && !hp && c->mode == QPSK_MODE_REFERENCE) {   // QPSK_SHAPE=4x3
+        const RxArgs ra{d_in, c->d_hist, c->d_ptab, c->d_ks, c->d_win[0], c->d_win[1], c->d_mi[0],
+                        c->d_mi[1], c->d_rt[0], c->d_rt[1], d_bits, d_valid, d_trace,
+                        reinterpret_cast<float2*>(d_soft), c->d_jobs, c->d_njobs + parity, c->nch, F,
+                        (unsigned)(c->frames & 0xffffffffu), c->jobs_cap, sh.roles, d_err, nullptr};
+        hipLaunchKernelGGL(rx43_kernel, dim3((unsigned)((c->nch + 4 * QK_GROUP - 1) / (4 * QK_GROUP))),
+                           dim3(64 * r43::kWaves), 0, s, ra);
+    } else if (sh.kind == Shape::k4x3) {
+        sh.kind = Shape::k4x2;   // 4x3 is reference mode without the head pre-pass only
+    }
+    if (sh.kind == Shape::k4x3) {
+    } else if (hp) {   // head pre-pass: every channel-frame's F_{n+1}, then the frame loop
         const size_t ncf = (size_t)c->nch * (size_t)F;
         hipLaunchKernelGGL(head_kernel, dim3((unsigned)((ncf + 3) / 4)), dim3(256), 0, s, d_in,
                            c->d_hist, c->d_ptab, c->d_heads, c->nch, F,
