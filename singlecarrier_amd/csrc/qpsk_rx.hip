@@ -79,6 +79,9 @@ constexpr int kDec = 296;
 #ifndef QPSK_HUNT_FILTER
 #define QPSK_HUNT_FILTER 1   // 1: bf16 first pass, exact chain only when the argmax is in doubt (qpsk_hunt.h)
 #endif
+#ifndef QPSK_FIR_WAIT
+#define QPSK_FIR_WAIT 1   // the FIRs: one lgkmcnt(0) per sample batch, not one per sample (0: A/B knob)
+#endif
 #ifndef QPSK_DYNPRIO
 // dynamic issue priority of the dual-chain back waves (rx_kernel): they train
 // at the highest priority unless another back wave waits for its fronts.
@@ -367,6 +370,11 @@ __device__ __forceinline__ void fir_dec752(int lane, int rt, const float2* M, fl
 #pragma unroll
             for (int j = 0; j < QPSK_FB; j++)
                 if (s0 + j < 69) v[j] = ld2nt(b + s0 + j);
+            if (QPSK_FIR_WAIT) {
+                __builtin_amdgcn_sched_barrier(0);
+                __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+                __builtin_amdgcn_sched_barrier(0);
+            }
 #pragma unroll
             for (int j = 0; j < QPSK_FB; j++) {
                 const int s = s0 + j;
@@ -439,6 +447,11 @@ __device__ __forceinline__ void fir_dec(int lane, int rt, const float2* M, float
 #pragma unroll
             for (int j = 0; j < FB; j++)
                 if (s0 + j < 59) v[j] = ld2nt(b + s0 + j);
+            if (QPSK_FIR_WAIT) {   // one wait per batch instead of one per sample
+                __builtin_amdgcn_sched_barrier(0);
+                __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+                __builtin_amdgcn_sched_barrier(0);
+            }
 #pragma unroll
             for (int j = 0; j < FB; j++) {
                 const int s = s0 + j;
@@ -475,6 +488,11 @@ __device__ __forceinline__ void fir_head_at(int lane, const float2* H, float2* o
                 const float4 q = *reinterpret_cast<const float4*>(b + s0 + j);
                 v[j] = f2{q.x, q.y};
                 v[j + 1] = f2{q.z, q.w};
+            }
+            if (QPSK_FIR_WAIT) {
+                __builtin_amdgcn_sched_barrier(0);
+                __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+                __builtin_amdgcn_sched_barrier(0);
             }
 #pragma unroll
             for (int j = 0; j < 10; j++) {
@@ -1901,7 +1919,10 @@ __device__ __attribute__((noinline)) void front_role() {
             fir_dec<QPSK_FB43, true>(fresh_lane(lane), rt - rt0, M, dec);
             fir_head_at(fresh_lane(lane), M + kHc, dec + QK_NDEC);
             wave_lds_sync();
-            const int mi = hunt<0>(fresh_lane(lane), M, dec, sBT);
+#ifdef QPSK_STAMPS
+            unsigned long long st_acc[16] = {};   // the 4x3 kernel is not stamped
+#endif
+            const int mi = hunt<0>(fresh_lane(lane), M, dec, sBT FACC_ARG);
             if (c + 1 < nlive)   // the next channel, after the FIR and hunt: pf is live across neither
                 prefetch(srcs(a, ch + 1, n), lane, sRt[gi][p][idx + 1] & ~1, pf);
             if (lane == 0) sMi[gi][p ^ 1][idx] = mi;
