@@ -82,6 +82,9 @@ constexpr int kDec = 296;
 #ifndef QPSK_FIR_WAIT
 #define QPSK_FIR_WAIT 1   // the FIRs: one lgkmcnt(0) per sample batch, not one per sample (0: A/B knob)
 #endif
+#ifndef QPSK_QDMUL
+#define QPSK_QDMUL 1   // quad step: rotated h times its column mask as v_mul_f32_dpp (qd_mul); 0: A/B knob
+#endif
 #ifndef QPSK_DYNPRIO
 // dynamic issue priority of the dual-chain back waves (rx_kernel): they train
 // at the highest priority unless another back wave waits for its fronts.
@@ -1021,6 +1024,15 @@ __device__ __forceinline__ float qdf(float v) {
 }
 template <int CTRL>
 __device__ __forceinline__ f2 qd2(f2 v) { return f2{qdf<CTRL>(v.x), qdf<CTRL>(v.y)}; }
+// qd2<CTRL>(v) * m as two v_mul_f32_dpp (the moves fold into the products);
+// the empty asm keeps the products scalar, else they pack into a v_pk_mul_f32
+// that takes no DPP source and the two moves stay
+template <int CTRL>
+__device__ __forceinline__ f2 qd_mul(f2 v, float m) {
+    float x = qdf<CTRL>(v.x) * m, y = qdf<CTRL>(v.y) * m;
+    if (QPSK_QDMUL) asm("" : "+v"(x), "+v"(y));
+    return f2{x, y};
+}
 
 struct QKal {
     f2 R[4];      // R[d-1] = u[c][c+d]
@@ -1139,24 +1151,21 @@ __device__ __forceinline__ float qstep(QKal& k, const f2& X0, const f2& X1, cons
         G = G + cmulc(g, B1);
     }
     {   // column c+2 (lane c+1); none for row 3
-        const f2 hr = qd2<qd::kRot3>(h);
-        const f2 hd = hr * m2;
+        const f2 hd = qd_mul<qd::kRot3>(h, m2);
         const f2 gd = qd2<qd::kRot3>(g);
         const f2 B1 = k.R[1];
         k.R[1] = B1 + cmulc(hd, G);
         G = G + cmulc(gd, B1);
     }
     {   // column c+3 (lane c+2); none for rows 2, 3
-        const f2 hr = qd2<qd::kRot2>(h);
-        const f2 hd = hr * m3;
+        const f2 hd = qd_mul<qd::kRot2>(h, m3);
         const f2 gd = qd2<qd::kRot2>(g);
         const f2 B1 = k.R[2];
         k.R[2] = B1 + cmulc(hd, G);
         G = G + cmulc(gd, B1);
     }
     {   // column c+4 (lane c+3); row 0 only
-        const f2 hr = qd2<qd::kRot1>(h);
-        const f2 hd = hr * m4;
+        const f2 hd = qd_mul<qd::kRot1>(h, m4);
         const f2 B1 = k.R[3];
         k.R[3] = B1 + cmulc(hd, G);
         G = G + cmulc(gr, B1);
