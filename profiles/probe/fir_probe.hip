@@ -1,7 +1,7 @@
 // FIR issue-rate probe: the front's fir_dec / fir_head alone, NW waves per CU
 // (one workgroup per CU), every wave filtering its own LDS block REPS times.
 // Prints cycles per call per wave (s_memtime = shader clock) for 1..4 waves
-// per SIMD.  Built by profiles/probe/Makefile against the product source.
+// per SIMD.  Built by profiles/probe/build.sh against the product source.
 #include "../../singlecarrier_amd/csrc/qpsk_rx.hip"
 #include <cstdio>
 #include <vector>
