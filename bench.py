@@ -679,8 +679,11 @@ def main():
                              f"{host['cgroup_cpu_quota']}), slowest {tmx:.1f} s", **host}
 
     if drop_in is not None and cpu is not None:
-        # the reference's time per frame on one core, from the baseline just timed
-        drop_in["reference_us_per_frame"] = round(FRAME / cpu["value"], 1)
+        # the CPU receiver's time per frame on one core, from the baseline just
+        # timed, under the name of what was timed: the unmodified reference, or
+        # (reference not built) the oracle's port
+        key = "reference_us_per_frame" if cpu["kind"] == "reference" else "port_us_per_frame"
+        drop_in[key] = round(FRAME / cpu["value"], 1)
     if rank == 0:
         ch_total = total_ch
         out = {

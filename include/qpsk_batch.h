@@ -42,7 +42,9 @@ enum {
                              nch * nframes >= 2^28 in one call: 1 TB of input) */
     QPSK_ENOMEM = -2,     /* device or host allocation failed */
     QPSK_ENODEV = -3,     /* no such HIP device */
-    /* -4 is QPSK_EBUSY (qpsk_stream.h) */
+    QPSK_EBUSY = -4,      /* qpsk_stream_acquire() with every slot in flight, or
+                             qpsk_rx_reset() / qpsk_rx_state_load() on a stream's
+                             context while chunks are pending: retrieve first */
     QPSK_ESTALL = -5,     /* a device-side progress wait of rx_kernel's dual-chain
                              shapes exceeded its bound (~0.1 s): the outputs of
                              the calls since the previous check are undefined.
@@ -77,13 +79,47 @@ enum {
 qpsk_ctx *qpsk_rx_create(int device, int nch, int *err);
 qpsk_ctx *qpsk_rx_create_mode(int device, int nch, int mode, int *err);
 void qpsk_rx_destroy(qpsk_ctx *ctx);
-/* Back to the initial state (all channels), as after qpsk_rx_create. */
+/* Back to the initial state (all channels), as after qpsk_rx_create.  Waits
+ * for the context's calls in flight first (they read the state it clears).
+ * On the context of a qpsk_stream (qpsk_stream_ctx) it returns QPSK_EBUSY
+ * while the stream has chunks submitted and not retrieved: drain the stream
+ * (qpsk_stream_retrieve until qpsk_stream_pending is 0), then reset. */
 int qpsk_rx_reset(qpsk_ctx *ctx);
 int qpsk_rx_channels(const qpsk_ctx *ctx);
 /* QPSK_MODE_* of the context. */
 int qpsk_rx_mode(const qpsk_ctx *ctx);
 /* Frames received so far by every channel of the context. */
 uint64_t qpsk_rx_frames(const qpsk_ctx *ctx);
+
+/* Per-channel state checkpoint / resume.  Between frames the
+ * reference carries, per channel, rx_timing (src/qpsk.c:53), the decimated
+ * symbols D_{n-1} and the sample history in its statics (decimated_frame /
+ * input_frame, src/qpsk.c:40-42) and the descrambler register
+ * (src/scramble.c:41-42, a function of the frame index).  The context holds
+ * the equivalent per channel in device memory: the history of the last two
+ * frames, the next frame's equalizer window (dec[mi .. mi+166]) with its
+ * preamble position, and rx_timing; the frame index is the context's.
+ *
+ *   qpsk_rx_state_size(n)        bytes of a snapshot of n channels
+ *   qpsk_rx_state_save(ctx, c0, n, buf, size)
+ *                                channels [c0, c0 + n) -> buf (host memory)
+ *   qpsk_rx_state_load(ctx, c0, n, buf, size)
+ *                                buf -> channels [c0, c0 + n) of ctx
+ *
+ * A snapshot records the context's mode and frame index.  Loading it into a
+ * context of the same mode (on any device, in any process) continues those
+ * channels exactly where they stopped: demodulating 7 frames, saving,
+ * loading into a fresh context and demodulating 9 more gives the outputs of
+ * one 16-frame call.  The frame index is shared by all channels of a
+ * context: a context takes the snapshot's index when it has received no
+ * frame since create/reset (qpsk_rx_frames() == 0); otherwise the indices
+ * must be equal (QPSK_EINVAL).  Both calls wait for the context's calls in
+ * flight; on a stream's context they return QPSK_EBUSY while chunks are
+ * pending.  n snapshots' channel ranges may differ from the ones loaded into
+ * (channel c0 + i of the snapshot goes to channel c0' + i). */
+size_t qpsk_rx_state_size(int n);
+int qpsk_rx_state_save(qpsk_ctx *ctx, int c0, int n, void *buf, size_t size);
+int qpsk_rx_state_load(qpsk_ctx *ctx, int c0, int n, const void *buf, size_t size);
 
 /* Host-memory call: copies `in` to the device, demodulates nframes frames of
  * every channel, copies the results back and synchronises; returns

@@ -27,13 +27,13 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include "qpsk_batch.h"   /* qpsk_ctx, QPSK_E* (QPSK_EBUSY = -4) */
+
 #ifdef __cplusplus
 extern "C" {
 #endif
 
 typedef struct qpsk_stream qpsk_stream;
-
-enum { QPSK_EBUSY = -4 };   /* acquire with every slot in flight: retrieve first */
 
 qpsk_stream *qpsk_stream_create(int device, int nch, int frames, int nslot, int *err);
 /* the same with the receiver semantics `mode` (QPSK_MODE_*, qpsk_batch.h) */
@@ -51,11 +51,15 @@ int qpsk_stream_pending(const qpsk_stream *s);
  * when a device-side progress wait of that chunk's receive ran out: its
  * outputs are then undefined (the chunk counts as retrieved either way).  The
  * stall is sticky: every later chunk starts from the per-channel state the
- * stalled one left, so it is reported QPSK_ESTALL too, until qpsk_rx_reset()
- * on qpsk_stream_ctx(s); the stall also reaches that context's own
+ * stalled one left, so it is reported QPSK_ESTALL too -- every chunk submitted
+ * before the next qpsk_rx_reset() on qpsk_stream_ctx(s).  A chunk's epoch is
+ * taken when it is submitted, and the reset itself is refused (QPSK_EBUSY)
+ * while chunks are pending, so a chunk that ran on the stalled state can
+ * never come back QPSK_OK.  The stall also reaches the context's own
  * qpsk_rx_sync(). */
 int qpsk_stream_retrieve(qpsk_stream *s, const uint8_t **bits, const uint8_t **valid);
-/* the stream's receiver (e.g. for qpsk_rx_frames / qpsk_rx_reset between streams) */
+/* the stream's receiver (e.g. for qpsk_rx_frames, or qpsk_rx_reset between
+ * streams once qpsk_stream_pending(s) is 0: it returns QPSK_EBUSY before) */
 struct qpsk_ctx *qpsk_stream_ctx(qpsk_stream *s);
 
 /* One channel's outputs -> reference records: 496 bytes per valid frame.

@@ -143,6 +143,10 @@ def lib():
         L.qpsk_fft_twiddle_table.restype = None
         L.qpsk_fft_twiddle_table.argtypes = [i32, i32, vp]
         L.qpsk_fft_perm_table.argtypes = [i32, vp]
+        L.qpsk_rx_state_size.restype = C.c_size_t
+        L.qpsk_rx_state_size.argtypes = [i32]
+        L.qpsk_rx_state_save.argtypes = [vp, i32, i32, vp, C.c_size_t]
+        L.qpsk_rx_state_load.argtypes = [vp, i32, i32, vp, C.c_size_t]
         L.cnormf.restype = C.c_float
         L.cnormf.argtypes = [_CF]   # _Complex float == {float, float} in one SSE reg (SysV)
         _lib = L
@@ -159,7 +163,8 @@ SYMBOLS = ["qpsk_rx_create", "qpsk_rx_create_mode", "qpsk_rx_mode", "qpsk_rx_des
            "qpsk_tx_phase_table", "qpsk_stream_create", "qpsk_stream_create_mode", "qpsk_stream_destroy",
            "qpsk_stream_acquire", "qpsk_stream_submit", "qpsk_stream_pending",
            "qpsk_stream_retrieve", "qpsk_stream_ctx", "qpsk_records", "qpsk_fft_alloc",
-           "qpsk_fft_free", "qpsk_fft_device", "qpsk_fft"]
+           "qpsk_fft_free", "qpsk_fft_device", "qpsk_fft", "qpsk_rx_state_size",
+           "qpsk_rx_state_save", "qpsk_rx_state_load"]
 
 
 def _check(rc: int) -> None:
@@ -213,6 +218,22 @@ class Receiver:
     @property
     def frames(self) -> int:
         return int(lib().qpsk_rx_frames(self._h))
+
+    def state_save(self, c0: int = 0, n: int | None = None) -> bytes:
+        """Snapshot of channels [c0, c0 + n) (qpsk_rx_state_save): the carried
+        per-channel state and the frame index, as bytes."""
+        n = self.nch - c0 if n is None else n
+        buf = np.zeros(int(lib().qpsk_rx_state_size(n)), np.uint8)
+        _check(lib().qpsk_rx_state_save(self._h, c0, n, _ptr(buf), buf.size))
+        return buf.tobytes()
+
+    def state_load(self, snap: bytes, c0: int = 0, n: int | None = None) -> None:
+        """Load a snapshot of n channels into channels [c0, c0 + n)
+        (qpsk_rx_state_load)."""
+        buf = np.frombuffer(snap, np.uint8)
+        if n is None:
+            n = int(np.frombuffer(snap[20:24], np.int32)[0])   # StateHdr.n
+        _check(lib().qpsk_rx_state_load(self._h, c0, n, _ptr(buf), buf.size))
 
     def timing(self, on: bool = True) -> None:
         """Enable per-call step-kernel span events (see qpsk_rx_timing_collect)."""

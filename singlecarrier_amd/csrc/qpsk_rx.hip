@@ -67,9 +67,6 @@ constexpr int kDec = 296;
 #ifndef QPSK_RX_ATTR
 #define QPSK_RX_ATTR   // A/B: e.g. __attribute__((amdgpu_num_vgpr(128))) to price a 4-wave budget
 #endif
-#ifndef QPSK_FIR_SB
-#define QPSK_FIR_SB 0   // 1: scheduling barrier after each FIR batch (register pressure A/B knob)
-#endif
 #ifndef QPSK_FRESH
 #define QPSK_FRESH 0   // 1: recompute the prefetch/mixer per-lane constants at each use (register A/B knob)
 #endif
@@ -436,10 +433,8 @@ __device__ __forceinline__ int fft_hunt(int lane, float2* M, const float2* dec, 
 
 // RRC (src/fir.c:36-42), outputs accumulated in tap order.  Decimated outputs
 // D[o] = fir_out[5o + rt] (model A): lane l makes o = 3l..3l+2
-// from the 59 samples M[15l + rt + s], read in batches.
-// FB samples per LDS batch; SB: a scheduling barrier after each batch (the
-// 4x3 front: bounds the samples in flight at its 128-VGPR budget)
-template <int FB = QPSK_FB, bool SB = QPSK_FIR_SB != 0>
+// from the 59 samples M[15l + rt + s], read in batches of FB samples.
+template <int FB = QPSK_FB>
 __device__ __forceinline__ void fir_dec(int lane, int rt, const float2* M, float2* dec) {
     if (lane < 63) {
         const float2* b = M + 15 * lane + rt;
@@ -464,7 +459,6 @@ __device__ __forceinline__ void fir_dec(int lane, int rt, const float2* M, float
                     if (s < 59 && k >= 0 && k < QK_NTAPS) y[m] = y[m] + v[j] * QK_RRC[k];
                 }
             }
-            if (SB) __builtin_amdgcn_sched_barrier(0);   // keep the next batch's loads behind this one
         }
 #pragma unroll
         for (int m = 0; m < 3; m++)
@@ -1425,7 +1419,7 @@ __global__ void __launch_bounds__(256) rx_data_kernel(const float4* jobs, unsign
 template <int G, int FP, int MODE, bool DUAL, int W, bool QUAD>
 constexpr int kBackWavesOf = DUAL ? 2 * G * (QUAD ? W / 16 : 1) : G;
 
-// waves per SIMD = ceil(waves / 4): 3 (<= 168 VGPRs) for the 12-wave shapes, 2 for 1x4
+// waves per SIMD = ceil(waves / 4): 3 (<= 168 VGPRs) for the 12-wave shapes
 template <int G, int FP, int MODE, bool DUAL, int W, bool QUAD>
 constexpr int kWavesOf = kBackWavesOf<G, FP, MODE, DUAL, W, QUAD> + G * FP;
 
@@ -1761,214 +1755,6 @@ __global__ void __launch_bounds__((64 * kWavesOf<G, FP, MODE, DUAL, W, QUAD>),
     }
 }
 
-// ---------------------------------------------------------------- 4x3 (C3 at 4 waves per SIMD)
-// rx43_kernel: 4 groups x (1 lane back + 3 fronts) = 16 waves, 4 per SIMD
-// (<= 128 VGPRs), one workgroup per CU; reference mode only (QPSK_SHAPE=4x3).
-// The 4x2 pipeline (one __syncthreads() per frame) with two changes that let
-// twelve fronts fit:
-// - the roles are separate functions (noinline): each is register-allocated
-//   on its own (compiled together in one kernel body both spill at 128 VGPRs,
-//   DESIGN.md round-4 item 2); they read the kernel argument block through the
-//   kernarg pointer (wave-uniform, scalar loads) and the LDS state as
-//   namespace-scope arrays;
-// - compact front input: the decimated FIR reads M[rt .. rt + 983] only, so a
-//   front mixes [rt0, rt0 + 986) (rt0 = rt & ~1) and the 152-sample head: 569
-//   two-sample items instead of 696, 9.1 KB of LDS per front; one dec buffer
-//   (the window is stored before the next channel's FIR).  The prefetch of a
-//   channel needs its rx_timing: the next channel of the frame is fetched after
-//   the current one's FIR, the frame's first channel after the frame barrier.
-#ifndef QPSK_FB43
-#define QPSK_FB43 8   // FIR samples per LDS batch in the 4x3 front (A/B knob)
-#endif
-namespace r43 {
-constexpr int kG = 4, kFP = 3, kFW = kG * kFP, kWaves = kG + kFW;
-constexpr int kMc = 1138;                    // float2: D part [rt0, rt0 + 986) ++ head [1240, 1392)
-constexpr int kHc = 986;                     // the head part's offset in Mc
-constexpr int kItems = kMc / 2;              // 569 two-sample items
-constexpr int kPfC = (kItems + 63) / 64;     // 9 per lane
-__shared__ __attribute__((aligned(16))) float2 sP[QK_FRAME];
-__shared__ __attribute__((aligned(16))) float2 sM[kFW][kMc];
-__shared__ __attribute__((aligned(16))) float2 sDec[kFW][kDec];
-__shared__ int sMi[kG][2][QK_GROUP], sRt[kG][2][QK_GROUP];
-__shared__ __attribute__((aligned(16))) float sBT[kHuntTab];
-
-// the launch's argument block, copied to LDS by the kernel (a called function
-// receives no kernarg segment pointer), read back wave-uniform (SGPRs)
-__shared__ RxArgs sArgs;
-static_assert(sizeof(RxArgs) % 4 == 0, "RxArgs as dwords");
-__device__ __forceinline__ RxArgs kargs() {
-    RxArgs r;
-    int* d = reinterpret_cast<int*>(&r);
-    const int* s = reinterpret_cast<const int*>(&sArgs);
-#pragma unroll
-    for (int i = 0; i < (int)(sizeof(RxArgs) / 4); i++) d[i] = __builtin_amdgcn_readfirstlane(s[i]);
-    return r;
-}
-
-// item d = lane + 64 i of the compact input: two samples at M index k (the
-// 4x2 front's M: k < 48 x_{n-2}[1832 + k], k < 1240 x_{n-1}[k - 48], k < 1288
-// x_{n-1}[1832 + k - 1240], else x_n[k - 1288]); returns the frame (0: n-2,
-// 1: n-1, 2: n) or -1, and the sample index t
-template <int i>
-__device__ __forceinline__ int item(int lane, int rt0, int& t) {
-    const int d = lane + 64 * i;
-    int k;
-    if (i < 7) k = rt0 + 2 * d;
-    else if (i == 7) k = d < 493 ? rt0 + 2 * d : 1240 + 2 * (d - 493);
-    else {
-        if (d >= kItems) { t = 0; return -1; }
-        k = 1240 + 2 * (d - 493);
-    }
-    if (i == 0 && k < 48) { t = 1832 + k; return 0; }   // rt < 48 only (rx_timing 3 before a first valid frame)
-    if (i < 7 || (i == 7 && d < 493)) { t = k - 48; return 1; }
-    if (k < 1288) { t = 1832 + (k - 1240); return 1; }
-    t = k - 1288;
-    return 2;
-}
-
-template <int i>
-__device__ __forceinline__ void load_item(const Src& s, int lane, int rt0, int& r) {
-    int t;
-    const int f = item<i>(lane, rt0, t);
-    if (f >= 0) r = *reinterpret_cast<const int*>((f == 0 ? s.xm2 : f == 1 ? s.xm1 : s.x0) + t);
-}
-template <int... I>
-__device__ __forceinline__ void prefetch_seq(const Src& s, int lane, int rt0, int (&r)[kPfC],
-                                             std::integer_sequence<int, I...>) {
-    (load_item<I>(s, lane, rt0, r[I]), ...);
-}
-__device__ __forceinline__ void prefetch(const Src& s, int lane, int rt0, int (&r)[kPfC]) {
-    prefetch_seq(s, fresh_lane(lane), rt0, r, std::make_integer_sequence<int, kPfC>{});
-}
-
-// mix_item of the 4x2 front on the compact item map: (-1)^G P[t] x 2^-14,
-// frame g-1 negated when NO
-template <int i, bool NO>
-__device__ __forceinline__ void mix_item(int lane, int rt0, int r, float2* M) {
-    int t;
-    const int f = item<i>(lane, rt0, t);
-    if (f < 0) return;
-    const float4 p = *reinterpret_cast<const float4*>(sP + t);
-    const float v0 = (float)(int16_t)(r & 0xffff);
-    const float v1 = (float)(int16_t)(r >> 16);
-    float4 o;
-    if (i >= 1 && i <= 7) {   // every lane's item is from frame g-1
-        o = NO ? make_float4((-p.x) * v0, (-p.y) * v0, (-p.z) * v1, (-p.w) * v1)
-               : make_float4(p.x * v0, p.y * v0, p.z * v1, p.w * v1);
-    } else {
-        const float sg = ((f == 1) == NO) ? -1.0f : 1.0f;   // exact sign flip
-        o = make_float4((sg * p.x) * v0, (sg * p.y) * v0, (sg * p.z) * v1, (sg * p.w) * v1);
-    }
-    *reinterpret_cast<float4*>(M + 2 * (lane + 64 * i)) = o;
-}
-template <bool NO, int... I>
-__device__ __forceinline__ void mix_seq(int lane, int rt0, const int (&r)[kPfC], float2* M,
-                                        std::integer_sequence<int, I...>) {
-    (mix_item<I, NO>(lane, rt0, r[I], M), ...);
-}
-__device__ __forceinline__ void mix(int lane, int rt0, const int (&r)[kPfC], unsigned g, float2* M) {
-    constexpr auto kSeq = std::make_integer_sequence<int, kPfC>{};
-    lane = fresh_lane(lane);
-    if (((g - 1u) & 1u) != 0) mix_seq<true>(lane, rt0, r, M, kSeq);   // frame g-1 odd
-    else mix_seq<false>(lane, rt0, r, M, kSeq);
-}
-
-// the back role (lane = channel): the 4x2 back on this kernel's LDS state
-__device__ __attribute__((noinline)) void back_role() {
-    const RxArgs a = kargs();
-    const int lane = __lane_id();
-    const int gi = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int ch = ((int)blockIdx.x * kG + gi) * QK_GROUP + lane;
-    const bool live = ch < a.nch;
-    const bool any = ((int)blockIdx.x * kG + gi) * QK_GROUP < a.nch;
-    if (((a.roles >> 4) & 3) == 2) __builtin_amdgcn_s_setprio(2);
-    for (int n = 0; n < a.F; n++) {
-        const int p = n & 1;
-        if (any && (a.roles & 1)) {
-            const int rt = sRt[gi][p][lane];
-            back_frame(a, live ? ch : 0, live, n, sMi[gi][p][lane], [=] { return rt; },
-                       win_of(a, a.g0 + (unsigned)n) + (size_t)(live ? ch : 0) * kWinStride,
-                       &sRt[gi][p ^ 1][lane], [] {});
-        } else {
-            sRt[gi][p ^ 1][lane] = sRt[gi][p][lane];
-        }
-        __syncthreads();
-    }
-    if (live) {   // per-channel state after the call's last frame
-        const unsigned ge = a.g0 + (unsigned)a.F;
-        mi_of(a, ge)[ch] = sMi[gi][a.F & 1][lane];
-        rt_of(a, ge)[ch] = sRt[gi][a.F & 1][lane];
-    }
-}
-
-// the front role: channels [cbeg, cbeg + 21 or 22) of its group, one at a time
-__device__ __attribute__((noinline)) void front_role() {
-    const RxArgs a = kargs();
-    const int lane = __lane_id();
-    const int f = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) - kG;
-    const int gi = f / kFP, fl = f % kFP;
-    const int cbeg = 21 * fl, cnt = fl == kFP - 1 ? QK_GROUP - 21 * (kFP - 1) : 21;
-    const int ch0 = ((int)blockIdx.x * kG + gi) * QK_GROUP + cbeg;
-    const int nlive = max(0, min(cnt, a.nch - ch0));
-    float2* M = sM[f];
-    float2* dec = sDec[f];
-    const bool on = (a.roles & 2) != 0 && nlive > 0;
-    if (((a.roles >> 4) & 3) == 1) __builtin_amdgcn_s_setprio(2);
-    int pf[kPfC];
-    for (int n = 0; n < a.F; n++) {
-        const int p = n & 1;
-        const unsigned g = a.g0 + (unsigned)n;
-        float2* wout = win_of(a, g + 1u);
-        if (on) prefetch(srcs(a, ch0, n), lane, sRt[gi][p][cbeg] & ~1, pf);
-        for (int c = 0; on && c < nlive; c++) {
-            const int ch = ch0 + c, idx = cbeg + c;
-            const int rt = sRt[gi][p][idx], rt0 = rt & ~1;
-            mix(lane, rt0, pf, g, M);
-            wave_lds_sync();
-            fir_dec<QPSK_FB43, true>(fresh_lane(lane), rt - rt0, M, dec);
-            fir_head_at(fresh_lane(lane), M + kHc, dec + QK_NDEC);
-            wave_lds_sync();
-#ifdef QPSK_STAMPS
-            unsigned long long st_acc[16] = {};   // the 4x3 kernel is not stamped
-#endif
-            const int mi = hunt<0>(fresh_lane(lane), M, dec, sBT FACC_ARG);
-            if (c + 1 < nlive)   // the next channel, after the FIR and hunt: pf is live across neither
-                prefetch(srcs(a, ch + 1, n), lane, sRt[gi][p][idx + 1] & ~1, pf);
-            if (lane == 0) sMi[gi][p ^ 1][idx] = mi;
-            store_window(fresh_lane(lane), mi, dec, wout + (size_t)ch * kWinStride);
-            wave_lds_sync();
-        }
-        __syncthreads();
-    }
-    carry_history<0>(a.in, a.hist, a.F, ch0, nlive, lane);
-}
-}  // namespace r43
-
-__global__ void __launch_bounds__(64 * r43::kWaves, 4) rx43_kernel(const RxArgs args) {
-    using namespace r43;
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    constexpr int kBlock = 64 * kWaves;
-    for (int i = threadIdx.x; i < QK_FRAME / 2; i += kBlock)
-        reinterpret_cast<float4*>(sP)[i] = reinterpret_cast<const float4*>(args.ptab)[i];
-#if QPSK_HUNT_FILTER
-    qhunt::bconst_h_lds(threadIdx.x, kBlock, sBT);
-#else
-    qhunt::bconst_lds(threadIdx.x, kBlock, sBT);
-#endif
-    if (wave < kG) {   // per-channel state of the groups at the call's first frame
-        const int ch = ((int)blockIdx.x * kG + wave) * QK_GROUP + lane;
-        if (ch < args.nch) {
-            sMi[wave][0][lane] = mi_of(args, args.g0)[ch];
-            sRt[wave][0][lane] = rt_of(args, args.g0)[ch];
-        }
-    }
-    if (threadIdx.x == 0) sArgs = args;
-    __syncthreads();
-    if (wave < kG) back_role();
-    else front_role();
-}
-
 // ---------------------------------------------------------------- host side
 
 float bits2f(uint32_t u) {
@@ -1981,7 +1767,7 @@ float bits2f(uint32_t u) {
 
 // rx_kernel instantiations (pick_shape below)
 struct Shape {
-    enum Kind { k4x2, k2x4d, k1x8d16, k1x8d32, k1x8d64, k1x8q16, k1x8q32, k1x4q16, k1x4q32, k1x4q64, k4x3 };
+    enum Kind { k4x2, k2x4d, k1x8d64, k1x8q16, k1x8q32 };
     int kind;
     int roles;
 };
@@ -2030,8 +1816,6 @@ struct qpsk_ctx {
     int ncu = 256;              // compute units of the device
     int shape = -1;             // Shape::Kind forced by QPSK_SHAPE (A/B runs); -1: by batch size
     int width = 0;              // dual-chain group width forced by QPSK_WIDTH; 0: by batch size
-    int quad = -1;              // quad-per-channel backs forced on/off by QPSK_QUAD; -1: by width
-    int fronts = 0;             // front waves of the quad shapes forced by QPSK_FRONTS (4 | 8); 0: by width
     int prio = -1;              // issue priority forced by QPSK_PRIO (0 none, 1 front, 2 back)
     bool headpass = false;      // QPSK_HEADPASS: the FIR-head pre-pass (reference mode only)
     float2* d_heads = nullptr;  // its outputs, [nch][F][102] for the largest call
@@ -2045,6 +1829,7 @@ struct qpsk_ctx {
     uint64_t epoch = 0;         // qpsk_rx_reset() count (qpsk_rx_epoch)
     int stall_calls = -1;       // QPSK_DEBUG_STALL=first: the stall only in the first launch; -1: every call
     uint64_t launches = 0;      // calls launched over the context's life (qpsk_rx_reset keeps it)
+    const qpsk_stream* owner = nullptr;   // the stream this context belongs to, if any
 };
 
 extern "C" int qpsk_rx_timing_split(qpsk_ctx* c, float* ms_rx, float* ms_data, int* frames);
@@ -2101,7 +1886,12 @@ static int ctx_alloc(qpsk_ctx* c) {
 
 extern "C" int qpsk_rx_reset(qpsk_ctx* c) {
     if (!c) return QPSK_EINVAL;
+    // a stream's chunks in flight run on the state cleared here (and one that
+    // stalled must keep its epoch): refuse until the stream is drained
+    if (c->owner && qpsk_stream_pending(c->owner) > 0) return QPSK_EBUSY;
     HCHECK(hipSetDevice(c->device));
+    // calls in flight on other streams read and write the state cleared here
+    if (c->called) HCHECK(hipEventSynchronize(c->done));
     const size_t ns = nslot(c);
     HCHECK(hipMemsetAsync(c->d_hist, 0, sizeof(int16_t) * ns * 2 * QK_FRAME, c->stream));
     HCHECK(hipMemsetAsync(c->d_njobs, 0, sizeof(unsigned) * 2, c->stream));
@@ -2125,6 +1915,7 @@ extern "C" int qpsk_rx_reset(qpsk_ctx* c) {
 }
 
 int* qpsk_rx_err_word(qpsk_ctx* c) { return c ? c->d_err : nullptr; }
+void qpsk_rx_set_owner(qpsk_ctx* c, const qpsk_stream* s) { if (c) c->owner = s; }
 uint64_t qpsk_rx_epoch(const qpsk_ctx* c) { return c ? c->epoch : 0; }
 
 static void ctx_free(qpsk_ctx* c) {
@@ -2216,13 +2007,11 @@ extern "C" qpsk_ctx* qpsk_rx_create_mode(int device, int nch, int mode, int* err
         const int v = atoi(w);
         c->width = (v == 16 || v == 32 || v == 64) ? v : 0;
     }
-    if (const char* qv = getenv("QPSK_QUAD")) c->quad = atoi(qv) != 0;
-    if (const char* fv = getenv("QPSK_FRONTS")) c->fronts = atoi(fv) == 4 ? 4 : atoi(fv) == 8 ? 8 : 0;
     if (const char* hv = getenv("QPSK_HEADPASS")) c->headpass = atoi(hv) != 0 && mode == QPSK_MODE_REFERENCE;
     if (const char* pv = getenv("QPSK_PRIO"))
         c->prio = !strcmp(pv, "none") ? 0 : !strcmp(pv, "front") ? 1 : !strcmp(pv, "back") ? 2 : -1;
     if (const char* sh = getenv("QPSK_SHAPE")) {
-        c->shape = !strcmp(sh, "4x2") ? Shape::k4x2 : !strcmp(sh, "4x3") ? Shape::k4x3
+        c->shape = !strcmp(sh, "4x2") ? Shape::k4x2
                  : !strcmp(sh, "2x4d") ? Shape::k2x4d
                  : !strcmp(sh, "1x8") ? Shape::k1x8d64 : -1;
     }
@@ -2254,6 +2043,92 @@ extern "C" qpsk_ctx* qpsk_rx_create_mode(int device, int nch, int mode, int* err
     return c;
 }
 
+// ---------------------------------------------------------------- state snapshots
+// qpsk_batch.h qpsk_rx_state_*: the per-channel state the kernels carry from
+// one call to the next, for the context's frame index G (the next frame):
+// the history int16 [2][1880] (frames G-2, G-1: carry_history), window G's
+// row float2 [168] with mi_G, and rt_G, the last three in the arrays of
+// parity G & 1 (rx_kernel reads mi_of / rt_of / win_of (g0) at a call's start
+// and writes parity g0 + F at its end).  Layout: a 64-byte header, then the
+// four fields channel-major, each as one contiguous block.
+namespace {
+constexpr char kStateMagic[8] = {'Q', 'P', 'S', 'K', 'S', 'T', 'A', '1'};
+struct StateHdr {
+    char magic[8];
+    uint32_t version, hdr_bytes;
+    int32_t mode, n;
+    uint64_t frame;
+    uint32_t hist_bytes, win_bytes;   // per channel
+    uint8_t pad[24];
+};
+static_assert(sizeof(StateHdr) == 64, "state header");
+constexpr size_t kHistB = sizeof(int16_t) * 2 * QK_FRAME, kWinB = sizeof(float2) * kWinStride;
+constexpr size_t kChanB = kHistB + kWinB + 2 * sizeof(int);
+}  // namespace
+
+extern "C" size_t qpsk_rx_state_size(int n) { return n < 1 ? 0 : sizeof(StateHdr) + (size_t)n * kChanB; }
+
+// the checks both directions share; waits for the context's calls in flight
+static int state_begin(qpsk_ctx* c, int c0, int n, const void* buf, size_t size) {
+    if (!c || !buf || n < 1 || c0 < 0 || c0 > c->nch - n || size < qpsk_rx_state_size(n)) return QPSK_EINVAL;
+    if (c->owner && qpsk_stream_pending(c->owner) > 0) return QPSK_EBUSY;
+    HCHECK(hipSetDevice(c->device));
+    if (c->called) HCHECK(hipEventSynchronize(c->done));
+    return QPSK_OK;
+}
+
+extern "C" int qpsk_rx_state_save(qpsk_ctx* c, int c0, int n, void* buf, size_t size) {
+    int r = state_begin(c, c0, n, buf, size);
+    if (r != QPSK_OK) return r;
+    StateHdr h{};
+    memcpy(h.magic, kStateMagic, sizeof h.magic);
+    h.version = 1;
+    h.hdr_bytes = sizeof h;
+    h.mode = c->mode;
+    h.n = n;
+    h.frame = c->frames;
+    h.hist_bytes = (uint32_t)kHistB;
+    h.win_bytes = (uint32_t)kWinB;
+    char* o = static_cast<char*>(buf);
+    memcpy(o, &h, sizeof h);
+    o += sizeof h;
+    const int p = (int)(c->frames & 1u);
+    const size_t nn = (size_t)n;
+    HCHECK(hipMemcpyAsync(o, c->d_hist + (size_t)c0 * 2 * QK_FRAME, nn * kHistB, hipMemcpyDeviceToHost, c->stream));
+    o += nn * kHistB;
+    HCHECK(hipMemcpyAsync(o, c->d_win[p] + (size_t)c0 * kWinStride, nn * kWinB, hipMemcpyDeviceToHost, c->stream));
+    o += nn * kWinB;
+    HCHECK(hipMemcpyAsync(o, c->d_mi[p] + c0, nn * sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    o += nn * sizeof(int);
+    HCHECK(hipMemcpyAsync(o, c->d_rt[p] + c0, nn * sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HCHECK(hipStreamSynchronize(c->stream));
+    return QPSK_OK;
+}
+
+extern "C" int qpsk_rx_state_load(qpsk_ctx* c, int c0, int n, const void* buf, size_t size) {
+    int r = state_begin(c, c0, n, buf, size);
+    if (r != QPSK_OK) return r;
+    StateHdr h;
+    memcpy(&h, buf, sizeof h);
+    if (memcmp(h.magic, kStateMagic, sizeof h.magic) != 0 || h.version != 1 || h.hdr_bytes != sizeof h ||
+        h.n != n || h.mode != c->mode || h.hist_bytes != kHistB || h.win_bytes != kWinB)
+        return QPSK_EINVAL;
+    if (c->frames != h.frame && c->frames != 0) return QPSK_EINVAL;   // one frame index per context
+    const char* o = static_cast<const char*>(buf) + sizeof h;
+    const int p = (int)(h.frame & 1u);
+    const size_t nn = (size_t)n;
+    HCHECK(hipMemcpyAsync(c->d_hist + (size_t)c0 * 2 * QK_FRAME, o, nn * kHistB, hipMemcpyHostToDevice, c->stream));
+    o += nn * kHistB;
+    HCHECK(hipMemcpyAsync(c->d_win[p] + (size_t)c0 * kWinStride, o, nn * kWinB, hipMemcpyHostToDevice, c->stream));
+    o += nn * kWinB;
+    HCHECK(hipMemcpyAsync(c->d_mi[p] + c0, o, nn * sizeof(int), hipMemcpyHostToDevice, c->stream));
+    o += nn * sizeof(int);
+    HCHECK(hipMemcpyAsync(c->d_rt[p] + c0, o, nn * sizeof(int), hipMemcpyHostToDevice, c->stream));
+    HCHECK(hipStreamSynchronize(c->stream));
+    c->frames = h.frame;
+    return QPSK_OK;
+}
+
 extern "C" void qpsk_rx_destroy(qpsk_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
@@ -2271,12 +2146,16 @@ extern "C" uint64_t qpsk_rx_frames(const qpsk_ctx* c) { return c ? c->frames : 0
 //   2 groups per CU: 2x4 with dual-chain backs (11% faster at 32,768 channels,
 //     profiles/r01_dual_ab.txt);
 //   1 group per CU: 1x8 dual-chain, at the narrowest group width (16/32/64
-//     channels) that still fits the batch in one wave of workgroups; at
-//     W = 64 with back priority and 2 channels moved off each front wave that
+//     channels) that still fits the batch in one wave of workgroups: quad
+//     backs at W = 16 / 32, lane backs at W = 64 (quad backs there need 16
+//     waves, whose 128-VGPR budget spills the front: profiles/r02_quad_ab.txt)
+//     with back priority and 2 channels moved off each front wave that
 //     shares a SIMD with a back wave (-3%, profiles/r01_split_ab.txt).
 // QPSK_SHAPE (4x2 | 2x4d | 1x8) and QPSK_WIDTH force a shape for tests and A/B
-// runs.  Measured and dropped (records in profiles/): 4x1d, 2x4 and 1x8 with
-// single back waves, the early-terminated flow kernel (r01_flow_ab.txt).
+// runs.  Measured and dropped (records in profiles/, DESIGN.md "Measured and
+// not kept"): 4x1d, 2x4 and 1x8 with single back waves, the early-terminated
+// flow kernel (r01_flow_ab.txt), lane backs at W = 16 / 32, one front per SIMD
+// (1x4) and the 4x3 C3 shape (round 5 removed the last three from the build).
 static Shape pick_shape(const qpsk_ctx* c) {
     Shape sh{c->shape, c->roles};
     if (sh.kind < 0)
@@ -2286,20 +2165,9 @@ static Shape pick_shape(const qpsk_ctx* c) {
         const int W = c->width > 0 ? c->width
                     : (size_t)c->nch <= (size_t)16 * c->ncu ? 16
                     : (size_t)c->nch <= (size_t)32 * c->ncu ? 32 : 64;
-        // quad backs need W / 16 back waves per chain: at W = 64 that is 16
-        // waves per workgroup, whose 128-VGPR budget spills the front; the
-        // lane-per-channel back stays there (profiles/r02_quad_ab.txt)
-        // (1x4 -- one front per SIMD, QPSK_FRONTS=4 -- leaves room for the 8 quad back
-        // waves of W = 64: 12 waves)
-        const bool f4 = c->fronts == 4;
-        const bool quad = (W <= 32 || f4) && (c->quad >= 0 ? c->quad != 0 : true);
-        if (quad) {
-            sh.kind = W == 16 ? (f4 ? Shape::k1x4q16 : Shape::k1x8q16)
-                    : W == 32 ? (f4 ? Shape::k1x4q32 : Shape::k1x8q32) : Shape::k1x4q64;
-        } else {
-            sh.kind = W == 16 ? Shape::k1x8d16 : W == 32 ? Shape::k1x8d32 : Shape::k1x8d64;
-            if (W == 64) sh.roles = (sh.roles & ~((3 << 4) | (15 << 16))) | (2 << 4) | (2 << 16);
-        }
+        if (W == 16) sh.kind = Shape::k1x8q16;
+        else if (W == 32) sh.kind = Shape::k1x8q32;
+        else sh.roles = (sh.roles & ~((3 << 4) | (15 << 16))) | (2 << 4) | (2 << 16);
     }
     if (c->prio >= 0) sh.roles = (sh.roles & ~(3 << 4)) | (c->prio << 4);
     return sh;
@@ -2372,30 +2240,14 @@ int qpsk_rx_launch(qpsk_ctx* c, const int16_t* d_in, int F, uint8_t* d_bits, uin
     do {                                                                                       \
         switch (sh.kind) {                                                                     \
             case Shape::k2x4d: QPSK_LAUNCH(2, 4, MM, true, 64, false, HH); break;              \
-            case Shape::k1x8d16: QPSK_LAUNCH(1, 8, MM, true, 16, false, HH); break;            \
-            case Shape::k1x8d32: QPSK_LAUNCH(1, 8, MM, true, 32, false, HH); break;            \
             case Shape::k1x8d64: QPSK_LAUNCH(1, 8, MM, true, 64, false, HH); break;            \
             case Shape::k1x8q16: QPSK_LAUNCH(1, 8, MM, true, 16, true, HH); break;             \
             case Shape::k1x8q32: QPSK_LAUNCH(1, 8, MM, true, 32, true, HH); break;             \
-            case Shape::k1x4q16: QPSK_LAUNCH(1, 4, MM, true, 16, true, HH); break;             \
-            case Shape::k1x4q32: QPSK_LAUNCH(1, 4, MM, true, 32, true, HH); break;             \
-            case Shape::k1x4q64: QPSK_LAUNCH(1, 4, MM, true, 64, true, HH); break;             \
             default: QPSK_LAUNCH(4, 2, MM, false, 64, false, HH); break;                       \
         }                                                                                      \
     } while (0)
 #define QPSK_LAUNCH_MODE(MM) QPSK_LAUNCH_SHAPES(MM, false)
-    if (sh.kind == Shape::k4x3 && !hp && c->mode == QPSK_MODE_REFERENCE) {   // QPSK_SHAPE=4x3
-        const RxArgs ra{d_in, c->d_hist, c->d_ptab, c->d_ks, c->d_win[0], c->d_win[1], c->d_mi[0],
-                        c->d_mi[1], c->d_rt[0], c->d_rt[1], d_bits, d_valid, d_trace,
-                        reinterpret_cast<float2*>(d_soft), c->d_jobs, c->d_njobs + parity, c->nch, F,
-                        (unsigned)(c->frames & 0xffffffffu), c->jobs_cap, sh.roles, d_err, nullptr};
-        hipLaunchKernelGGL(rx43_kernel, dim3((unsigned)((c->nch + 4 * QK_GROUP - 1) / (4 * QK_GROUP))),
-                           dim3(64 * r43::kWaves), 0, s, ra);
-    } else if (sh.kind == Shape::k4x3) {
-        sh.kind = Shape::k4x2;   // 4x3 is reference mode without the head pre-pass only
-    }
-    if (sh.kind == Shape::k4x3) {
-    } else if (hp) {   // head pre-pass: every channel-frame's F_{n+1}, then the frame loop
+    if (hp) {   // head pre-pass: every channel-frame's F_{n+1}, then the frame loop
         const size_t ncf = (size_t)c->nch * (size_t)F;
         hipLaunchKernelGGL(head_kernel, dim3((unsigned)((ncf + 3) / 4)), dim3(256), 0, s, d_in,
                            c->d_hist, c->d_ptab, c->d_heads, c->nch, F,
@@ -2564,21 +2416,19 @@ extern "C" int qpsk_rx_batch(qpsk_ctx* c, const int16_t* in, int F, uint8_t* bit
     HCHECK(hipMemcpyAsync(h + g.bits, d + g.bits, nbv, hipMemcpyDeviceToHost, c->stream));
     if (trace) HCHECK(hipMemcpyAsync(h + g.trace, d + g.trace, ntr, hipMemcpyDeviceToHost, c->stream));
     if (soft) HCHECK(hipMemcpyAsync(h + g.soft, d + g.soft, nso, hipMemcpyDeviceToHost, c->stream));
-    // the error word: every call on this context is ordered on its stream
-    // (qpsk_rx_sync's contract), so reading it behind this call's kernels and
-    // clearing it only when set needs no atomic exchange
-    HCHECK(hipMemcpyAsync(c->s_pin_err, c->d_err, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    // the error word, taken in one atomic exchange behind this call's kernels
+    // (as qpsk_rx_sync): a stream on this context (qpsk_stream_ctx) ORs its
+    // slots' stalls into the same word from another HIP stream, and a read
+    // followed by a separate clear could lose one merged in between
+    hipLaunchKernelGGL(err_take_kernel, dim3(1), dim3(64), 0, c->stream, c->d_err);
+    HCHECK(hipGetLastError());
+    HCHECK(hipMemcpyAsync(c->s_pin_err, c->d_err + 1, sizeof(int), hipMemcpyDeviceToHost, c->stream));
     HCHECK(hipStreamSynchronize(c->stream));
     memcpy(bits, h + g.bits, cf * QK_NBITS);
     memcpy(valid, h + g.valid, cf);
     if (trace) memcpy(trace, h + g.trace, ntr);
     if (soft) memcpy(soft, h + g.soft, nso);
-    if (*c->s_pin_err != 0) {
-        HCHECK(hipMemsetAsync(c->d_err, 0, sizeof(int), c->stream));
-        HCHECK(hipStreamSynchronize(c->stream));
-        return QPSK_ESTALL;
-    }
-    return QPSK_OK;
+    return *c->s_pin_err != 0 ? QPSK_ESTALL : QPSK_OK;
 }
 
 #ifdef QPSK_STAMPS

@@ -19,3 +19,9 @@ int* qpsk_rx_err_word(qpsk_ctx* c);
 // Bumped by every qpsk_rx_reset(): a stream keeps reporting a stall for every
 // later chunk until the per-channel state it corrupted has been reset.
 uint64_t qpsk_rx_epoch(const qpsk_ctx* c);
+
+// The stream that owns a context (qpsk_stream_create_mode): qpsk_rx_reset()
+// and qpsk_rx_state_load() refuse with QPSK_EBUSY while it has chunks pending.
+struct qpsk_stream;
+void qpsk_rx_set_owner(qpsk_ctx* c, const qpsk_stream* s);
+extern "C" int qpsk_stream_pending(const qpsk_stream* s);

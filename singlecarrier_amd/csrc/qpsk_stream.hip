@@ -26,6 +26,7 @@ struct Slot {
     int* d_err = nullptr;        // the chunk's device error word (progress-wait stalls)
     int* h_err = nullptr;        // pinned copy, read by qpsk_stream_retrieve
     hipEvent_t copied = nullptr, received = nullptr, done = nullptr;
+    uint64_t epoch = 0;          // qpsk_rx_epoch() when the chunk was submitted
 };
 
 int herr(hipError_t e) { return e == hipSuccess ? QPSK_OK : QPSK_EHIP - (int)e; }
@@ -44,8 +45,10 @@ struct qpsk_stream {
     Slot slot[kMaxSlots];
     uint64_t acquired = 0, submitted = 0, retrieved = 0;
     // A stalled chunk leaves every channel's carried state (rx_timing, windows,
-    // history) undefined, so every later chunk is reported QPSK_ESTALL too,
-    // until qpsk_rx_reset() on the stream's context (a new epoch).
+    // history) undefined, so every later chunk of the same epoch (submitted
+    // before the next qpsk_rx_reset() on the stream's context) is reported
+    // QPSK_ESTALL too.  Chunks are retrieved in submission order, so when a
+    // chunk is retrieved every earlier chunk's stall is known.
     bool stalled = false;
     uint64_t stall_epoch = 0;
 };
@@ -119,6 +122,7 @@ extern "C" qpsk_stream* qpsk_stream_create_mode(int device, int nch, int frames,
     s->frames = frames;
     s->nslot = nslot;
     s->rx = qpsk_rx_create_mode(device, nch, mode, err);
+    if (s->rx) qpsk_rx_set_owner(s->rx, s);
     int r = s->rx ? stream_alloc(s) : *err;
     if (r != QPSK_OK) {
         stream_free(s);
@@ -182,6 +186,7 @@ extern "C" int qpsk_stream_submit(qpsk_stream* s) {
     SCHECK(hipMemcpyAsync(q.h_valid, q.d_valid, cf, hipMemcpyDeviceToHost, s->s_d2h));
     SCHECK(hipMemcpyAsync(q.h_err, q.d_err, sizeof(int), hipMemcpyDeviceToHost, s->s_d2h));
     SCHECK(hipEventRecord(q.done, s->s_d2h));
+    q.epoch = qpsk_rx_epoch(s->rx);
     s->submitted++;
     return QPSK_OK;
 }
@@ -199,15 +204,15 @@ extern "C" int qpsk_stream_retrieve(qpsk_stream* s, const uint8_t** bits, const 
     *valid = q.h_valid;
     s->retrieved++;
     // a progress wait of this chunk's receive ran out: its bits are undefined,
-    // and so are those of every later chunk, which start from the state it
-    // left (the slot is released all the same)
-    const uint64_t ep = qpsk_rx_epoch(s->rx);
-    if (s->stalled && ep != s->stall_epoch) s->stalled = false;   // reset since
+    // and so are those of every later chunk of its epoch, which start from the
+    // state it left (the slot is released all the same).  The epoch is the
+    // chunk's own, taken at submit: a chunk submitted before a reset that ran
+    // on the stalled state stays ESTALL, one submitted after it is clean.
     if (*q.h_err != 0) {
         s->stalled = true;
-        s->stall_epoch = ep;
+        s->stall_epoch = q.epoch;
     }
-    return s->stalled ? QPSK_ESTALL : QPSK_OK;
+    return (s->stalled && q.epoch == s->stall_epoch) ? QPSK_ESTALL : QPSK_OK;
 }
 
 extern "C" qpsk_ctx* qpsk_stream_ctx(qpsk_stream* s) { return s ? s->rx : nullptr; }

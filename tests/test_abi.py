@@ -37,6 +37,17 @@ def test_library_exports_every_declared_symbol():
     assert set(sc.SYMBOLS) >= declared
 
 
+def test_state_snapshot_size():
+    """qpsk_rx_state_size (host only): a 64-byte header plus, per channel, the
+    two-frame sample history (2 x 1880 int16), the next frame's equalizer
+    window (168 float2), its preamble position and rx_timing."""
+    L = sc.lib()
+    assert L.qpsk_rx_state_size(0) == 0
+    per = 2 * 1880 * 2 + 168 * 8 + 4 + 4
+    assert L.qpsk_rx_state_size(1) == 64 + per
+    assert L.qpsk_rx_state_size(65536) == 64 + 65536 * per
+
+
 def test_code_object_targets_gfx950():
     data = open(sc.LIB_PATH, "rb").read()
     assert b"gfx950" in data
