@@ -38,6 +38,10 @@
 
 #include "qpsk_consts.h"
 
+#ifndef QPSK_HUNT_OVERLAP
+#define QPSK_HUNT_OVERLAP 0   // 1: W's wave reduction after the MFMAs are issued (A/B knob)
+#endif
+
 namespace qhunt {
 
 constexpr int kSteps = 36;          // K = 144 = 36 x 4
@@ -310,7 +314,8 @@ __device__ __forceinline__ float wave_sum_f32(float v) {
 }
 
 // bf16 images of T (as store_t: T[j] = (RN(dr - di), RN(di + dr)), j < 255);
-// lane l writes j = 4l .. 4l+3 of each image.  Returns W (wave-uniform).
+// lane l writes j = 4l .. 4l+3 of each image.  Returns this lane's part of W
+// (W = the wave sum of the parts, wave_sum_f32).
 __device__ __forceinline__ float store_h(int lane, const float2* dec, char* H) {
     const float4* d4 = reinterpret_cast<const float4*>(dec + 4 * lane);
     const float4 p = d4[0], q = d4[1];
@@ -345,7 +350,7 @@ __device__ __forceinline__ float store_h(int lane, const float2* dec, char* H) {
         for (int c = 0; c < 4; c++)
             *reinterpret_cast<uint4*>(H + himg(c) + 512 + 16 * lane) = make_uint4(0u, 0u, 0u, 0u);
     }
-    return wave_sum_f32(w);
+    return w;
 }
 
 // The bf16 pass: this lane's D fragment (lags lag_lo / lag_hi, as correlate)
@@ -446,13 +451,24 @@ template <typename WaveMax>
 __device__ __forceinline__ int hunt_index(int lane, const float2* dec, float* S, const float* TB,
                                           WaveMax wave_max, bool& fb) {
     char* H = reinterpret_cast<char*>(S);
-    const float W = store_h(lane, dec, H);
+    const float w = store_h(lane, dec, H);
     fb = false;
+#if QPSK_HUNT_OVERLAP
+    // the MFMAs first, W's DPP reduction in their shadow (neither waits for
+    // the other; the all-zero test only needs W before the pick)
+    lds_sync();
+    const f4 acc = correlate_h(lane, H, TB);
+    const float W = wave_sum_f32(w);
+    if (W == 0.0f) return 0;
+    const int pick = pick_h(lane, acc, W, wave_max);
+#else
+    const float W = wave_sum_f32(w);
     // an all-zero window (W sums non-negative terms: 0 only if every T is):
     // every sum is 0, so no lag exceeds the initial max and max_index stays 0
     if (W == 0.0f) return 0;
     lds_sync();
     const int pick = pick_h(lane, correlate_h(lane, H, TB), W, wave_max);
+#endif
     fb = pick < 0;
     if (!fb) return pick;
     lds_sync();   // the exact image overwrites H

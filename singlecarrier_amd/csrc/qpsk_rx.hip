@@ -82,6 +82,9 @@ constexpr int kDec = 296;
 #ifndef QPSK_QDMUL
 #define QPSK_QDMUL 1   // quad step: rotated h times its column mask as v_mul_f32_dpp (qd_mul); 0: A/B knob
 #endif
+#ifndef QPSK_RCP_PAIR
+#define QPSK_RCP_PAIR 1   // lane backs / data jobs: the reciprocals' Newton steps on pairs (0: A/B knob)
+#endif
 #ifndef QPSK_DYNPRIO
 // dynamic issue priority of the dual-chain back waves (rx_kernel): they train
 // at the highest priority unless another back wave waits for its fronts.
@@ -508,9 +511,23 @@ __device__ __forceinline__ int fft_hunt(int lane, float2* M, const float2* dec, 
 // RRC (src/fir.c:36-42), outputs accumulated in tap order.  Decimated outputs
 // D[o] = fir_out[5o + rt] (model A): lane l makes o = 3l..3l+2
 // from the 59 samples M[15l + rt + s], read in batches of FB samples.
+#ifndef QPSK_FIR_NOMASK
+#define QPSK_FIR_NOMASK 0   // 1: all 64 lanes filter and store (A/B knob, see fir_dec)
+#endif
+#ifndef QPSK_FIR_READ2
+#define QPSK_FIR_READ2 0    // 1: plain loads, which the compiler pairs into ds_read2_b64 (A/B knob)
+#endif
+__device__ __forceinline__ f2 ld2_fir(const float2* p) {
+    if (QPSK_FIR_READ2) return *reinterpret_cast<const f2*>(p);
+    return ld2nt(p);
+}
+// QPSK_FIR_NOMASK: lane 63 (and lane 62's third output) compute outputs past
+// D[187] from samples inside M (M[15 * 63 + rt + 58] < M[1259]) and store them
+// to dec[188 .. 191], which fir_head (or the head pre-pass copy) rewrites right
+// after in the same wave's program order: no exec-mask branch around the FIR.
 template <int FB = QPSK_FB>
 __device__ __forceinline__ void fir_dec(int lane, int rt, const float2* M, float2* dec) {
-    if (lane < 63) {
+    if (QPSK_FIR_NOMASK || lane < 63) {
         const float2* b = M + 15 * lane + rt;
         f2 y[3] = {{0.0f, 0.0f}, {0.0f, 0.0f}, {0.0f, 0.0f}};
 #pragma unroll
@@ -518,7 +535,7 @@ __device__ __forceinline__ void fir_dec(int lane, int rt, const float2* M, float
             f2 v[FB];
 #pragma unroll
             for (int j = 0; j < FB; j++)
-                if (s0 + j < 59) v[j] = ld2nt(b + s0 + j);
+                if (s0 + j < 59) v[j] = ld2_fir(b + s0 + j);
             if (QPSK_FIR_WAIT) {   // one wait per batch instead of one per sample
                 __builtin_amdgcn_sched_barrier(0);
                 __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
@@ -536,7 +553,7 @@ __device__ __forceinline__ void fir_dec(int lane, int rt, const float2* M, float
         }
 #pragma unroll
         for (int m = 0; m < 3; m++)
-            if (3 * lane + m < QK_NDEC) {
+            if (QPSK_FIR_NOMASK || 3 * lane + m < QK_NDEC) {
                 const f2 o = y[m] * QK_GAIN;
                 dec[3 * lane + m] = make_float2(o.x, o.y);
             }
@@ -800,7 +817,9 @@ __host__ __device__ constexpr int uix(int i, int j) { return j * (j - 1) / 2 + i
 // EXACT = false: `bmax` collects the bit pattern of the step's largest
 // reciprocal operand xs[4] (the callers test bmax <= bits(2^125) once per
 // frame or job: qk_rcp_in_range() for every step, a NaN or -x has larger bits).
-template <bool EXACT>
+// RP: the reciprocals' Newton steps on pairs (qk_rcp_pair; the lane back only:
+// in rx_data_kernel ROCm 7.2's greedy register allocator crashes on it)
+template <bool EXACT, bool RP = false>
 __device__ __forceinline__ float kal_gain(Kal& k, const f2 (&x)[5], unsigned& bmax) {
     const float E = QK_KAL_E, q = QK_KAL_Q;
     f2 f[5];
@@ -837,11 +856,16 @@ __device__ __forceinline__ float kal_gain(Kal& k, const f2 (&x)[5], unsigned& bm
     } else {
         // the one check: xs[0] >= E unless NaN, and a NaN reaches xs[4] too
         bmax = max(bmax, __float_as_uint(xs[4]));
-        // qk_rcp_fast on pairs: the two Newton FMAs of two divisors packed
-        // (the Newton steps as packed pairs crash ROCm 7.2's greedy register
-        // allocator in several of these kernels: kept scalar)
+        if (RP) {
+            // qk_rcp_fast with the Newton FMAs of two divisors as one packed
+            // FMA each (qk_rcp_pair: the same fmaf per half)
+            qk_rcp_pair(xs[0], xs[1], ys[0], ys[1]);
+            qk_rcp_pair(xs[2], xs[3], ys[2], ys[3]);
+            ys[4] = qk_rcp_fast(xs[4]);
+        } else {
 #pragma unroll
-        for (int j = 0; j < 5; j++) ys[j] = qk_rcp_fast(xs[j]);
+            for (int j = 0; j < 5; j++) ys[j] = qk_rcp_fast(xs[j]);
+        }
     }
     float y = ys[0];                                      // 6.19
     k.d[0] = k.d[0] * ((hq * (E + ht)) * y);              // 6.20 (both halves)
@@ -863,9 +887,9 @@ __device__ __forceinline__ float kal_gain(Kal& k, const f2 (&x)[5], unsigned& bm
 
 // update_eq (src/equalizer.c:25-40): the gain, then error *= kalman_y and
 // eq_i += error * conj(g_i)
-template <bool EXACT>
+template <bool EXACT, bool RP = false>
 __device__ __forceinline__ void update_eq(Kal& k, const f2 (&x)[5], f2 e, unsigned& bmax) {
-    const float y = kal_gain<EXACT>(k, x, bmax);
+    const float y = kal_gain<EXACT, RP>(k, x, bmax);
     e = e * y;                                            // error *= kalman_y
 #pragma unroll
     for (int i = 0; i < 5; i++) k.eq[i] = k.eq[i] + cmulc(e, k.g[i]);
@@ -991,7 +1015,7 @@ __device__ __forceinline__ int train(Kal& k, f2 (&x)[5], const f2* wp2, bool& ba
 #pragma unroll
         for (int t = 0; t < 5; t++) v = v + cmul(x[t], k.eq[t]);
         const float er = ref - v.x;                // conjf(ref - val) = (ref - vr, vi)
-        update_eq<EXACT>(k, x, f2{er, v.y}, bmax);
+        update_eq<EXACT, QPSK_RCP_PAIR != 0>(k, x, f2{er, v.y}, bmax);
         if (er * ref > 0.0f) matches++;
 #pragma unroll
         for (int t = 0; t < 4; t++) x[t] = x[t + 1];

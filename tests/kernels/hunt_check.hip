@@ -88,7 +88,7 @@ __global__ void __launch_bounds__(64) hunt_h_kernel(const float2* dec, float2* o
     const float2* d = dec + (size_t)blockIdx.x * 256;
     for (int j = lane; j < 256; j += 64) D[j] = d[j];
     __syncthreads();
-    const float W = qhunt::store_h(lane, D, reinterpret_cast<char*>(S));
+    const float W = qhunt::wave_sum_f32(qhunt::store_h(lane, D, reinterpret_cast<char*>(S)));
     qhunt::lds_sync();
     const qhunt::f4 acc = qhunt::correlate_h(lane, reinterpret_cast<const char*>(S), TB);
     float2* o = out + (size_t)blockIdx.x * QK_NLAG;

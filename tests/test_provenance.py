@@ -76,3 +76,29 @@ def test_record_of_another_workload_is_dropped(tmp_path):
     _write_records(str(tmp_path), cur, nch=8192)
     assert bench.pmc_record("pmc_traffic.json", 65536, 32, "reference", cur, root=str(tmp_path)) is None
     assert bench.pmc_record("pmc_traffic.json", 8192, 32, "dec752", cur, root=str(tmp_path)) is None
+
+
+def _make(*args):
+    import subprocess
+    inc = os.path.join(os.path.dirname(CSRC), "..", "include")
+    return subprocess.run(["make", "-s", "--no-print-directory", "-C", CSRC, f"INCDIR={os.path.abspath(inc)}",
+                           *args], capture_output=True, text=True)
+
+
+def test_variant_flags_change_the_hash_and_force_a_rebuild():
+    """a QPSK_VARIANT build must never keep the product's
+    hash, a plain `make` after it must rebuild the product object, and knobs
+    with quotes or spaces must hash as written (the flags reach the hash
+    through a file, not the shell's quoting)."""
+    _lib_built()
+    base = _make("khash").stdout.strip()
+    assert base == sc.kernel_hash()
+    var = _make("khash", "QPSK_VARIANT=-DQPSK_FIR_NOMASK=1").stdout.strip()
+    quoted = _make("khash", "QPSK_VARIANT=-DQPSK_RX_ATTR='__attribute__((amdgpu_num_vgpr(128)))'")
+    assert quoted.returncode == 0 and re.fullmatch(r"[0-9a-f]{16}", quoted.stdout.strip())
+    assert len({base, var, quoted.stdout.strip()}) == 3
+    # the object depends on a per-hash stamp: with the variant's flags the
+    # product object is out of date (dry run: nothing is built here)
+    dry = _make("-n", "QPSK_VARIANT=-DQPSK_FIR_NOMASK=1")
+    assert "qpsk_rx.hip" in dry.stdout and "QPSK_FIR_NOMASK" in dry.stdout
+    assert "qpsk_rx.hip" not in _make("-n").stdout
