@@ -39,7 +39,9 @@
 #include "qpsk_consts.h"
 
 #ifndef QPSK_HUNT_OVERLAP
-#define QPSK_HUNT_OVERLAP 0   // 1: W's wave reduction after the MFMAs are issued (A/B knob)
+// 1: W's wave reduction after the MFMAs are issued (C3 -0.4%, 8,192 channels
+// -0.8%, 16,384 +0.3%: profiles/r05_hov_ab_*.txt); 0: round 4's order (A/B knob)
+#define QPSK_HUNT_OVERLAP 1
 #endif
 
 namespace qhunt {

@@ -83,7 +83,10 @@ constexpr int kDec = 296;
 #define QPSK_QDMUL 1   // quad step: rotated h times its column mask as v_mul_f32_dpp (qd_mul); 0: A/B knob
 #endif
 #ifndef QPSK_RCP_PAIR
-#define QPSK_RCP_PAIR 1   // lane backs / data jobs: the reciprocals' Newton steps on pairs (0: A/B knob)
+// 1: the lane back's reciprocal Newton steps on pairs (A/B knob: 15 fewer
+// instructions per 4 steps, but 4 more spilled VGPRs in the 4x2 kernel and
+// +0.8% at C3, profiles/r05_knobs_ab.txt)
+#define QPSK_RCP_PAIR 0
 #endif
 #ifndef QPSK_DYNPRIO
 // dynamic issue priority of the dual-chain back waves (rx_kernel): they train
@@ -511,23 +514,9 @@ __device__ __forceinline__ int fft_hunt(int lane, float2* M, const float2* dec, 
 // RRC (src/fir.c:36-42), outputs accumulated in tap order.  Decimated outputs
 // D[o] = fir_out[5o + rt] (model A): lane l makes o = 3l..3l+2
 // from the 59 samples M[15l + rt + s], read in batches of FB samples.
-#ifndef QPSK_FIR_NOMASK
-#define QPSK_FIR_NOMASK 0   // 1: all 64 lanes filter and store (A/B knob, see fir_dec)
-#endif
-#ifndef QPSK_FIR_READ2
-#define QPSK_FIR_READ2 0    // 1: plain loads, which the compiler pairs into ds_read2_b64 (A/B knob)
-#endif
-__device__ __forceinline__ f2 ld2_fir(const float2* p) {
-    if (QPSK_FIR_READ2) return *reinterpret_cast<const f2*>(p);
-    return ld2nt(p);
-}
-// QPSK_FIR_NOMASK: lane 63 (and lane 62's third output) compute outputs past
-// D[187] from samples inside M (M[15 * 63 + rt + 58] < M[1259]) and store them
-// to dec[188 .. 191], which fir_head (or the head pre-pass copy) rewrites right
-// after in the same wave's program order: no exec-mask branch around the FIR.
 template <int FB = QPSK_FB>
 __device__ __forceinline__ void fir_dec(int lane, int rt, const float2* M, float2* dec) {
-    if (QPSK_FIR_NOMASK || lane < 63) {
+    if (lane < 63) {
         const float2* b = M + 15 * lane + rt;
         f2 y[3] = {{0.0f, 0.0f}, {0.0f, 0.0f}, {0.0f, 0.0f}};
 #pragma unroll
@@ -535,7 +524,7 @@ __device__ __forceinline__ void fir_dec(int lane, int rt, const float2* M, float
             f2 v[FB];
 #pragma unroll
             for (int j = 0; j < FB; j++)
-                if (s0 + j < 59) v[j] = ld2_fir(b + s0 + j);
+                if (s0 + j < 59) v[j] = ld2nt(b + s0 + j);
             if (QPSK_FIR_WAIT) {   // one wait per batch instead of one per sample
                 __builtin_amdgcn_sched_barrier(0);
                 __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
@@ -553,7 +542,7 @@ __device__ __forceinline__ void fir_dec(int lane, int rt, const float2* M, float
         }
 #pragma unroll
         for (int m = 0; m < 3; m++)
-            if (QPSK_FIR_NOMASK || 3 * lane + m < QK_NDEC) {
+            if (3 * lane + m < QK_NDEC) {
                 const f2 o = y[m] * QK_GAIN;
                 dec[3 * lane + m] = make_float2(o.x, o.y);
             }
@@ -2153,6 +2142,10 @@ extern "C" qpsk_ctx* qpsk_rx_create_mode(int device, int nch, int mode, int* err
         c->width = (v == 16 || v == 32 || v == 64) ? v : 0;
     }
     if (const char* hv = getenv("QPSK_HEADPASS")) c->headpass = atoi(hv) != 0 && mode == QPSK_MODE_REFERENCE;
+    if (const char* sv = getenv("QPSK_STAGGER")) {   // A/B: the 4x2 fronts' stagger, 512-cycle units
+        const int v = atoi(sv);
+        if (v >= 0 && v < 256) c->roles = (c->roles & ~(255 << 8)) | (v << 8);
+    }
     if (const char* pv = getenv("QPSK_PRIO"))
         c->prio = !strcmp(pv, "none") ? 0 : !strcmp(pv, "front") ? 1 : !strcmp(pv, "back") ? 2 : -1;
     if (const char* sh = getenv("QPSK_SHAPE")) {

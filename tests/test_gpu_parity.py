@@ -445,23 +445,25 @@ def _gpus():
     return torch.cuda.device_count()
 
 
-def test_state_snapshot_resumes_exactly():
+@pytest.mark.parametrize("mode", [sc.MODE_REFERENCE, sc.MODE_DEC752, sc.MODE_DEC752 | sc.MODE_FFT_HUNT])
+def test_state_snapshot_resumes_exactly(mode):
     """Checkpoint / resume (qpsk_rx_state_save / _load): 7 frames
     on context A, a snapshot, loaded into a fresh context B (the second GPU
     when there is one), 9 more frames there == one 16-frame call, bit for
     bit, soft symbols included; and == the oracle (the statics being carried
-    are src/qpsk.c:34-53 and src/scramble.c:41-42)."""
+    are src/qpsk.c:34-53 and src/scramble.c:41-42).  In every receiver mode
+    (dec752's front reads a longer history)."""
     nch, nf, cut = 300, 16, 7
     x = oracle.synth(150, nch, nf, 5.0)
-    whole = sc.Receiver(nch).demod(x, trace=True, soft=True)
-    bits, valid, tr = oracle.cpu_rx(x, trace=True)
+    whole = sc.Receiver(nch, mode=mode).demod(x, trace=True, soft=True)
+    bits, valid, tr = oracle.cpu_rx(x, trace=True, mode=mode)
     _assert_same(whole, bits, valid, tr)
-    a = sc.Receiver(nch)
+    a = sc.Receiver(nch, mode=mode)
     first = a.demod(np.ascontiguousarray(x[:, :cut]), trace=True, soft=True)
     snap = a.state_save()
     assert len(snap) == sc.lib().qpsk_rx_state_size(nch)
     a.close()
-    b = sc.Receiver(nch, device=1 if _gpus() > 1 else 0)
+    b = sc.Receiver(nch, device=1 if _gpus() > 1 else 0, mode=mode)
     b.state_load(snap)
     assert b.frames == cut
     rest = b.demod(np.ascontiguousarray(x[:, cut:]), trace=True, soft=True)
