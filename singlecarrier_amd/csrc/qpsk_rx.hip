@@ -84,8 +84,9 @@ constexpr int kDec = 296;
 #endif
 #ifndef QPSK_TRAIN_PRETAB
 // 1: the lane back's preamble signs as one scalar load per step from kPreTab
-// instead of ~6 scalar instructions of bit extraction (A/B knob)
-#define QPSK_TRAIN_PRETAB 0
+// instead of ~6 scalar instructions of bit extraction (967 -> 943 instructions
+// per 4 steps; C3 -0.3%, profiles/r05_pretab_data_ab.txt); 0: A/B knob
+#define QPSK_TRAIN_PRETAB 1
 #endif
 #ifndef QPSK_RCP_PAIR
 // 1: the lane back's reciprocal Newton steps on pairs (A/B knob: 15 fewer
@@ -1398,16 +1399,10 @@ struct JobX {
     }
 };
 
-#ifndef QPSK_DATA_SOFT_T
-#define QPSK_DATA_SOFT_T 0   // 1: rx_data_kernel's fast path without a soft-symbol test per step (A/B knob)
-#endif
 #ifndef QPSK_DATA_RING
 #define QPSK_DATA_RING 4   // job samples loaded this many steps ahead (1: one step; profiles/r02_data_ring_ab.txt)
 #endif
-// SOFT: the soft symbols are stored (a template flag, not a test of `so` in
-// every step: a branch per step splits the unrolled loop into one scheduling
-// region per step)
-template <bool EXACT, bool SOFT = true>
+template <bool EXACT>
 __device__ __forceinline__ void data_step(Kal& k, f2 (&x)[5], f2 nx, int s, unsigned long long& dib,
                                           float2* so, unsigned& bmax) {
     f2 sy = {0.0f, 0.0f};
@@ -1417,13 +1412,13 @@ __device__ __forceinline__ void data_step(Kal& k, f2 (&x)[5], f2 nx, int s, unsi
     const f2 cst = {dI ? -1.0f : 1.0f, dQ ? -1.0f : 1.0f};
     update_eq<EXACT>(k, x, (cst - sy) * 0.1f, bmax);
     dib |= (unsigned long long)(dQ | (dI << 1)) << (2 * s);
-    if (SOFT && so) so[s] = make_float2(sy.x, sy.y);
+    if (so) so[s] = make_float2(sy.x, sy.y);
 #pragma unroll
     for (int t = 0; t < 4; t++) x[t] = x[t + 1];
     x[4] = nx;
 }
 
-template <bool EXACT, bool SOFT = true>
+template <bool EXACT>
 __device__ __forceinline__ unsigned long long data_steps(Kal& k, f2 (&x)[5], const JobX xs,
                                                          float2* so, bool& bad) {
     unsigned long long dib = 0;
@@ -1441,12 +1436,12 @@ __device__ __forceinline__ unsigned long long data_steps(Kal& k, f2 (&x)[5], con
         for (int t = 0; t < R; t++) nxt[t] = xs[min(s0 + R + 5 + t, 34)];
 #pragma unroll
         for (int t = 0; t < R; t++)
-            if (s0 + t < QK_NDSYM) data_step<EXACT, SOFT>(k, x, cur[t], s0 + t, dib, so, bmax);
+            if (s0 + t < QK_NDSYM) data_step<EXACT>(k, x, cur[t], s0 + t, dib, so, bmax);
 #pragma unroll
         for (int t = 0; t < R; t++) cur[t] = nxt[t];
     }
 #else
-    for (int s = 0; s < QK_NDSYM; s++) data_step<EXACT, SOFT>(k, x, xs[min(s + 5, 34)], s, dib, so, bmax);
+    for (int s = 0; s < QK_NDSYM; s++) data_step<EXACT>(k, x, xs[min(s + 5, 34)], s, dib, so, bmax);
 #endif
     if (!EXACT) bad |= bmax > __float_as_uint(0x1p125f);
     return dib;
@@ -1460,10 +1455,7 @@ __device__ __forceinline__ unsigned long long data_steps(Kal& k, f2 (&x)[5], con
 // lanes for 31 of its 159 steps.  Jobs come from the call's rx_kernel in any
 // order; every output location is fixed by the job, so results do not depend
 // on it.
-#ifndef QPSK_DATA_WPE
-#define QPSK_DATA_WPE 0   // >0: rx_data_kernel at that many waves per SIMD (launch bounds; A/B knob)
-#endif
-__global__ void __launch_bounds__(256, QPSK_DATA_WPE) rx_data_kernel(const float4* jobs, unsigned long long jcap,
+__global__ void __launch_bounds__(256) rx_data_kernel(const float4* jobs, unsigned long long jcap,
                                                       unsigned* njobs,
                                                       const unsigned long long* ks_tab,
                                                       uint8_t* bits, float2* soft, int parity,
@@ -1482,13 +1474,7 @@ __global__ void __launch_bounds__(256, QPSK_DATA_WPE) rx_data_kernel(const float
         const unsigned long long ks = ks_tab[j.ks];
         float2* so = soft ? soft + j.cf * QK_NDSYM : nullptr;
         bool bad = force_exact != 0;
-#if QPSK_DATA_SOFT_T
-        // the common case (no soft symbols requested) without the store
-        unsigned long long dib = so ? data_steps<false, true>(j.k, x, xs, so, bad)
-                                    : data_steps<false, false>(j.k, x, xs, so, bad);
-#else
         unsigned long long dib = data_steps<false>(j.k, x, xs, so, bad);
-#endif
         if (__builtin_expect(bad, 0)) {   // recompute the job with IEEE division
             get_job(jobs, cap, off, j);
 #pragma unroll
@@ -1930,7 +1916,9 @@ struct Shape {
     int roles;
 };
 
-constexpr int kStagger = 12;   // front stagger, 512-cycle units (roles bits 8-15)
+// front stagger, 512-cycle units (roles bits 8-15): round 1 measured 12 as
+// -0.7%; on round 5's kernels 0 is -0.4% (profiles/r05_stagger_ab.txt)
+constexpr int kStagger = 0;
 // rx_data_kernel grid: persistent, 4 workgroups of 256 per CU (other geometries
 // measured within 2%, profiles/r01_data_ab.txt)
 constexpr int kDataGrid = 1024, kDataBlock = 256;
@@ -1967,7 +1955,8 @@ struct qpsk_ctx {
     int ev_frames[kEv] = {};
     int ev_n = 0;
     bool timing = false;
-    // roles + front issue priority + front stagger (12 x 512 cycles: -0.7%,
+    // roles + front issue priority + front stagger (0 since round 5; 12 x 512
+    // cycles was -0.7% in round 1,
     // profiles/r01_stagger_ab.txt); QPSK_ABLATE (profiling), QPSK_FORCE_EXACT /
     // QPSK_DEBUG_STALL (tests)
     int roles = 3 | (1 << 4) | (kStagger << 8);
