@@ -82,6 +82,9 @@ constexpr int kDec = 296;
 #ifndef QPSK_QDMUL
 #define QPSK_QDMUL 1   // quad step: rotated h times its column mask as v_mul_f32_dpp (qd_mul); 0: A/B knob
 #endif
+#ifndef QPSK_COMPACT_NEXT
+#define QPSK_COMPACT_NEXT 0   // 1: see rx_kernel's kCN (A/B knob)
+#endif
 #ifndef QPSK_TRAIN_PRETAB
 // 1: the lane back's preamble signs as one scalar load per step from kPreTab
 // instead of ~6 scalar instructions of bit extraction (967 -> 943 instructions
@@ -679,11 +682,10 @@ __device__ __forceinline__ int hunt(int lane, float2* M, const float2* dec, cons
 // correlation of dec_{n+1} = [D_n, F_{n+1}] and its argmax mi.
 // HP (QPSK_HEADPASS): F_{n+1} comes from the head pre-pass (head_kernel), at
 // `head` (global, 51 x 16 B), instead of the head FIR.
-// HOFF: where M holds the head's 152 samples (kM1; the compact layout of the
-// QPSK_FRONT_AB variants: kHc).
-template <int MODE, bool HP = false, int HOFF = kM1>
+// hoff: where M holds the head's 152 samples (kM1; the compact layout: kHc).
+template <int MODE, bool HP = false>
 __device__ __forceinline__ int front_channel(int lane, int rt, float2* M, float2* dec,
-                                             const float* BT, const float2* head FACC_PARAM) {
+                                             const float* BT, const float2* head, int hoff FACC_PARAM) {
 #ifdef QPSK_STAMPS
     unsigned long long ft0 = stamp_now();
 #endif
@@ -699,7 +701,7 @@ __device__ __forceinline__ int front_channel(int lane, int rt, float2* M, float2
     } else {
         fir_dec(lane, rt, M, dec);
         FSTAMP(0);
-        fir_head_at(lane, M + HOFF, dec + QK_NDEC);
+        fir_head_at(lane, M + hoff, dec + QK_NDEC);
     }
     wave_lds_sync();
     FSTAMP(1);
@@ -1539,6 +1541,9 @@ __global__ void __launch_bounds__((64 * kWavesOf<G, FP, MODE, DUAL, W, QUAD, AB>
     static_assert(!QUAD || (DUAL && G == 1 && W % 16 == 0), "quad backs: dual chain, one group");
     static_assert(AB == 0 || (!DUAL && MODE == 0 && !HP), "front A/B: the 4x2 reference kernel only");
     constexpr bool kCM = AB != 0;                       // compact front input, one dec buffer
+    // QPSK_COMPACT_NEXT: the 4x2 (non-dual) reference fronts mix the compact input
+    // for every channel but a frame's first
+    constexpr bool kCN = QPSK_COMPACT_NEXT && !DUAL && MODE == 0 && !HP && AB == 0;
     constexpr int kGroups = G, kFrontPer = FP;
     constexpr int kBackWaves = kBackWavesOf<G, FP, MODE, DUAL, W, QUAD, AB>;
     constexpr int kChainWaves = QUAD ? W / 16 : 1;     // back waves per frame chain and group
@@ -1740,7 +1745,7 @@ __global__ void __launch_bounds__((64 * kWavesOf<G, FP, MODE, DUAL, W, QUAD, AB>
                 wave_lds_sync();                                                                               \
                 STAMP(1);                                                                                      \
                 pmi = front_channel<MODE, HP>(lane, rt_s[gi][p][i0 + c], M, dcur, BT,                          \
-                                              a.heads + ((size_t)ch * a.F + n) * kHeadOut FACC_ARG);           \
+                                              a.heads + ((size_t)ch * a.F + n) * kHeadOut, kM1 FACC_ARG);      \
                 if (lane == 0) mi_s[gi][p ^ 1][i0 + c] = pmi;                                                  \
                 if (c + 1 == nl) store_window(lane, pmi, dcur, wout + (size_t)ch * kWinStride);                \
                 wave_lds_sync();                                                                               \
@@ -1846,7 +1851,7 @@ __global__ void __launch_bounds__((64 * kWavesOf<G, FP, MODE, DUAL, W, QUAD, AB>
                     if (c > 0) store_window(lane, pmi, dec, wout + (size_t)(ch - 1) * kWinStride);
                     if (c + 1 < nl) prefetch_c(srcs(a, ch + 1, n), lane, rt_s[gi][p][cb + c + 1] & ~1, pf);
                     wave_lds_sync();
-                    pmi = front_channel<MODE, false, kHc>(lane, rt - rt0, M, dec, BT, nullptr FACC_ARG);
+                    pmi = front_channel<MODE, false>(lane, rt - rt0, M, dec, BT, nullptr, kHc FACC_ARG);
                     if (lane == 0) mi_s[gi][p ^ 1][cb + c] = pmi;
                     if (c + 1 == nl) store_window(lane, pmi, dec, wout + (size_t)ch * kWinStride);
                     wave_lds_sync();
@@ -1874,18 +1879,29 @@ __global__ void __launch_bounds__((64 * kWavesOf<G, FP, MODE, DUAL, W, QUAD, AB>
             for (int c = 0; on && c < nlive; c++) {
                 const int ch = ch0 + c;
                 float2* dcur = decs[f][c % kDecBuf];
-                mix<DM>(lane, pf, g, P, M);
+                const int rt = rt_s[gi][p][cbeg + c];
+                // kCN (QPSK_COMPACT_NEXT): channels after the frame's first were
+                // prefetched with their rx_timing known, as the compact input
+                // (item_c: 569 items instead of 696); the first, fetched during
+                // the previous frame (rx_timing not decided yet), is the full one
+                const int rt0 = (kCN && c > 0) ? (rt & ~1) : 0;
+                if (kCN && c > 0) mix_c(lane, rt0, *reinterpret_cast<int(*)[kPfC]>(&pf[0]), g, P, M);
+                else mix<DM>(lane, pf, g, P, M);
                 STAMP(0);
                 if (c > 0) store_window(lane, pmi, decs[f][(c - 1) % kDecBuf], wout + (size_t)(ch - 1) * kWinStride);
                 {   // next channel of this frame, else the first of the next frame
                     const bool same = c + 1 < nlive;
-                    if (same || n + 1 < a.F)
+                    if (kCN && same)
+                        prefetch_c(srcs(a, ch + 1, n), lane, rt_s[gi][p][cbeg + c + 1] & ~1,
+                                   *reinterpret_cast<int(*)[kPfC]>(&pf[0]));
+                    else if (same || n + 1 < a.F)
                         prefetch<DM>(srcs(a, same ? ch + 1 : ch0, same ? n : n + 1), lane, pf);
                 }
                 wave_lds_sync();
                 STAMP(1);
-                pmi = front_channel<MODE, HP>(lane, rt_s[gi][p][cbeg + c], M, dcur, BT,
-                                              a.heads + ((size_t)ch * a.F + n) * kHeadOut FACC_ARG);
+                pmi = front_channel<MODE, HP>(lane, rt - rt0, M, dcur, BT,
+                                              a.heads + ((size_t)ch * a.F + n) * kHeadOut,
+                                              (kCN && c > 0) ? kHc : kM1 FACC_ARG);
                 if (lane == 0) mi_s[gi][p ^ 1][cbeg + c] = pmi;
                 if (c + 1 == nlive) store_window(lane, pmi, dcur, wout + (size_t)ch * kWinStride);
                 wave_lds_sync();
