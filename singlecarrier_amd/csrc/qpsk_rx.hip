@@ -26,6 +26,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <utility>
 
 #include "qpsk_batch.h"
@@ -1962,7 +1963,6 @@ struct qpsk_ctx {
     // memory (the per-frame drop-in qpsk_rx_frame is such a call)
     char* s_dev = nullptr;
     char* s_pin = nullptr;          // pinned, same layout; only while small
-    int* s_pin_err = nullptr;       // pinned: the error word, read after the call
     size_t s_frames = 0;
     // kernel-span accounting: events before rx_kernel, between the kernels, after
     // rx_data_kernel
@@ -2101,7 +2101,6 @@ static void ctx_free(qpsk_ctx* c) {
     }
     (void)hipFree(c->s_dev);
     (void)hipHostFree(c->s_pin);
-    (void)hipHostFree(c->s_pin_err);
     if (c->stream) (void)hipStreamDestroy(c->stream);
 }
 
@@ -2450,7 +2449,10 @@ int qpsk_rx_launch(qpsk_ctx* c, const int16_t* d_in, int F, uint8_t* d_bits, uin
 #undef QPSK_LAUNCH
     HCHECK(hipGetLastError());
     if (slot >= 0) HCHECK(hipEventRecord(c->ev[slot][1], s));
-    hipLaunchKernelGGL(rx_data_kernel, dim3(kDataGrid), dim3(kDataBlock), 0, s, c->d_jobs,
+    // at most one job per channel-frame: a small call (the per-frame drop-in
+    // qpsk_rx_frame is one job at most) launches only the workgroups it can use
+    const unsigned dgrid = (unsigned)std::min<size_t>(kDataGrid, (need + kDataBlock - 1) / kDataBlock);
+    hipLaunchKernelGGL(rx_data_kernel, dim3(dgrid), dim3(kDataBlock), 0, s, c->d_jobs,
                        (unsigned long long)c->jobs_cap, c->d_njobs, c->d_ks, d_bits,
                        reinterpret_cast<float2*>(d_soft), parity, c->roles & kForceExact);
     HCHECK(hipGetLastError());
@@ -2475,6 +2477,11 @@ namespace {
 // kernel between a read and a separate clear cannot be lost
 __global__ void err_take_kernel(int* err) {
     if (threadIdx.x == 0) err[1] = atomicExch(&err[0], 0);
+}
+// the same, the taken value stored at `to` (qpsk_rx_batch: inside the staging
+// block, so it comes back with the bits in one copy)
+__global__ void err_take_to_kernel(int* err, int* to) {
+    if (threadIdx.x == 0) *to = atomicExch(&err[0], 0);
 }
 }  // namespace
 
@@ -2534,15 +2541,16 @@ extern "C" int qpsk_rx_timing_collect(qpsk_ctx* c, float* ms, int* frames) {
 
 // byte offsets of the staging block for cf channel-frames
 struct Stage {
-    size_t in, bits, valid, trace, soft, end;
+    size_t in, bits, valid, err, trace, soft, end;
 };
 static Stage stage_of(size_t cf) {
     auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
     Stage g;
     g.in = 0;
     g.bits = up(sizeof(int16_t) * cf * QK_FRAME);
-    g.valid = g.bits + cf * QK_NBITS;   // bits and valid adjacent: one D2H
-    g.trace = up(g.valid + cf);
+    g.valid = g.bits + cf * QK_NBITS;   // bits, valid and the taken error word
+    g.err = (g.valid + cf + 3) & ~(size_t)3;   // adjacent: one D2H
+    g.trace = up(g.err + sizeof(int));
     g.soft = up(g.trace + sizeof(int32_t) * cf * 4);
     g.end = up(g.soft + sizeof(float) * cf * QK_NDSYM * 2);
     return g;
@@ -2561,7 +2569,6 @@ static int stage_grow(qpsk_ctx* c, size_t F) {
     const Stage g = stage_of(cf);
     HCHECK(hipMalloc(&c->s_dev, g.end));
     if (g.bits <= kPinnedStage) HCHECK(hipHostMalloc((void**)&c->s_pin, g.end, hipHostMallocDefault));
-    if (!c->s_pin_err) HCHECK(hipHostMalloc((void**)&c->s_pin_err, sizeof(int), hipHostMallocDefault));
     c->s_frames = F;
     return QPSK_OK;
 }
@@ -2580,7 +2587,7 @@ extern "C" int qpsk_rx_batch(qpsk_ctx* c, const int16_t* in, int F, uint8_t* bit
     // pinned: the caller's input is copied into the pinned image (a host memcpy)
     // and moves in one DMA, outputs come back in one; pageable otherwise
     char* h = pin ? c->s_pin : nullptr;
-    const size_t nin = sizeof(int16_t) * cf * QK_FRAME, nbv = cf * QK_NBITS + cf;
+    const size_t nin = sizeof(int16_t) * cf * QK_FRAME;
     const size_t ntr = sizeof(int32_t) * cf * 4, nso = sizeof(float) * cf * QK_NDSYM * 2;
     if (pin) memcpy(h + g.in, in, nin);
     HCHECK(hipMemcpyAsync(d + g.in, pin ? (const void*)(h + g.in) : (const void*)in, nin,
@@ -2597,22 +2604,26 @@ extern "C" int qpsk_rx_batch(qpsk_ctx* c, const int16_t* in, int F, uint8_t* bit
         if (soft) HCHECK(hipMemcpyAsync(soft, d + g.soft, nso, hipMemcpyDeviceToHost, c->stream));
         return qpsk_rx_sync(c);
     }
-    HCHECK(hipMemcpyAsync(h + g.bits, d + g.bits, nbv, hipMemcpyDeviceToHost, c->stream));
+    // the error word, taken in one atomic exchange behind this call's kernels
+    // (as qpsk_rx_sync: a stream on this context, qpsk_stream_ctx, ORs its
+    // slots' stalls into the same word from another HIP stream, and a read
+    // followed by a separate clear could lose one merged in between), into the
+    // staging block right after the valid flags: bits, flags and error word
+    // come back in one copy
+    hipLaunchKernelGGL(err_take_to_kernel, dim3(1), dim3(64), 0, c->stream, c->d_err,
+                       reinterpret_cast<int*>(d + g.err));
+    HCHECK(hipGetLastError());
+    HCHECK(hipMemcpyAsync(h + g.bits, d + g.bits, g.err + sizeof(int) - g.bits, hipMemcpyDeviceToHost, c->stream));
     if (trace) HCHECK(hipMemcpyAsync(h + g.trace, d + g.trace, ntr, hipMemcpyDeviceToHost, c->stream));
     if (soft) HCHECK(hipMemcpyAsync(h + g.soft, d + g.soft, nso, hipMemcpyDeviceToHost, c->stream));
-    // the error word, taken in one atomic exchange behind this call's kernels
-    // (as qpsk_rx_sync): a stream on this context (qpsk_stream_ctx) ORs its
-    // slots' stalls into the same word from another HIP stream, and a read
-    // followed by a separate clear could lose one merged in between
-    hipLaunchKernelGGL(err_take_kernel, dim3(1), dim3(64), 0, c->stream, c->d_err);
-    HCHECK(hipGetLastError());
-    HCHECK(hipMemcpyAsync(c->s_pin_err, c->d_err + 1, sizeof(int), hipMemcpyDeviceToHost, c->stream));
     HCHECK(hipStreamSynchronize(c->stream));
     memcpy(bits, h + g.bits, cf * QK_NBITS);
     memcpy(valid, h + g.valid, cf);
     if (trace) memcpy(trace, h + g.trace, ntr);
     if (soft) memcpy(soft, h + g.soft, nso);
-    return *c->s_pin_err != 0 ? QPSK_ESTALL : QPSK_OK;
+    int e;
+    memcpy(&e, h + g.err, sizeof e);
+    return e != 0 ? QPSK_ESTALL : QPSK_OK;
 }
 
 #ifdef QPSK_STAMPS
