@@ -13,6 +13,10 @@
 #   ab2       QPSK_FRONT_AB=2: 12 compact fronts, 3/SIMD, no back waves
 # Timing: bench.py's HIP events, R interleaved rounds; then one rocprofv3
 # counter pass per arm (LDS and wait counters).
+# The A/B kernels live in commit 868e9f0 (moved out of the product source after
+# the A/B); build the two variant libraries from it first:
+#   bash profiles/build_variant.sh ab1 868e9f0 -DQPSK_FRONT_AB=1
+#   bash profiles/build_variant.sh ab2 868e9f0 -DQPSK_FRONT_AB=2
 #   bash profiles/occ_ab.sh R TAG
 set -o pipefail
 R=${1:-3}; TAG=${2:-occ}

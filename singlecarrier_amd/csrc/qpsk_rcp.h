@@ -23,19 +23,6 @@ __device__ __forceinline__ float qk_rcp_fast(float x) {
     const float e = __builtin_fmaf(-x, r, 1.0f);
     return __builtin_fmaf(e, r, r);
 }
-// qk_rcp_fast of two operands with each Newton step as one v_pk_fma_f32 (IEEE
-// fma per half, the same two roundings as the scalar form)
-__device__ __forceinline__ void qk_rcp_pair(float a, float b, float& ya, float& yb) {
-    typedef float f2_ __attribute__((ext_vector_type(2)));
-    const f2_ x = {a, b};
-    const f2_ r = {__builtin_amdgcn_rcpf(a), __builtin_amdgcn_rcpf(b)};
-    const f2_ one = {1.0f, 1.0f};
-    f2_ e, y;
-    asm("v_pk_fma_f32 %0, %1, %2, %3 neg_lo:[1,0,0] neg_hi:[1,0,0]" : "=v"(e) : "v"(x), "v"(r), "s"(one));
-    asm("v_pk_fma_f32 %0, %1, %2, %2" : "=v"(y) : "v"(e), "v"(r));
-    ya = y.x;
-    yb = y.y;
-}
 __device__ __forceinline__ bool qk_rcp_in_range(float lo, float hi) {
     return lo >= 0x1p-125f && hi <= 0x1p125f;   // false for NaN
 }

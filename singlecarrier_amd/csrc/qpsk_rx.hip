@@ -83,20 +83,11 @@ constexpr int kDec = 296;
 #ifndef QPSK_QDMUL
 #define QPSK_QDMUL 1   // quad step: rotated h times its column mask as v_mul_f32_dpp (qd_mul); 0: A/B knob
 #endif
-#ifndef QPSK_COMPACT_NEXT
-#define QPSK_COMPACT_NEXT 0   // 1: see rx_kernel's kCN (A/B knob)
-#endif
 #ifndef QPSK_TRAIN_PRETAB
 // 1: the lane back's preamble signs as one scalar load per step from kPreTab
 // instead of ~6 scalar instructions of bit extraction (967 -> 943 instructions
 // per 4 steps; C3 -0.3%, profiles/r05_pretab_data_ab.txt); 0: A/B knob
 #define QPSK_TRAIN_PRETAB 1
-#endif
-#ifndef QPSK_RCP_PAIR
-// 1: the lane back's reciprocal Newton steps on pairs (A/B knob: 15 fewer
-// instructions per 4 steps, but 4 more spilled VGPRs in the 4x2 kernel and
-// +0.8% at C3, profiles/r05_knobs_ab.txt)
-#define QPSK_RCP_PAIR 0
 #endif
 #ifndef QPSK_DYNPRIO
 // dynamic issue priority of the dual-chain back waves (rx_kernel): they train
@@ -349,80 +340,6 @@ __device__ __forceinline__ void mix(int lane, const int (&r)[kPf<MODE>], unsigne
     if (QPSK_FRESH) lane = fresh_lane(lane);
     if (((g - 1u) & 1u) != 0) mix_seq<MODE, true>(lane, r, P, M, kSeq);   // frame g-1 odd
     else mix_seq<MODE, false>(lane, r, P, M, kSeq);
-}
-
-// ---------------------------------------------------------------- compact front input
-// QPSK_FRONT_AB variants only (the C3 occupancy A/B): the decimating
-// FIR reads M[rt .. rt + 984) only (D[187] = fir_out[935 + rt] uses M[935 + rt ..
-// 983 + rt]), so a front can mix [rt0, rt0 + 986) (rt0 = rt & ~1) plus the
-// head's 152 samples: 569 two-sample items instead of 696, 9.1 KB of LDS per
-// front instead of 11.1 (12 fronts fit one CU only so).  Item d = lane + 64 i:
-// M index k (the full layout's: k < 48 x_{n-2}[1832 + k], k < 1240
-// x_{n-1}[k - 48], k < 1288 x_{n-1}[1832 + k - 1240], else x_n[k - 1288]) ->
-// frame (0: n-2, 1: n-1, 2: n; -1: none) and sample index t.
-constexpr int kMc = 1138;                  // float2: [rt0, rt0 + 986) ++ head [1240, 1392)
-constexpr int kHc = 986;                   // the head's offset in the compact M
-constexpr int kItemsC = kMc / 2;           // 569
-constexpr int kPfC = (kItemsC + 63) / 64;  // 9 per lane
-template <int i>
-__device__ __forceinline__ int item_c(int lane, int rt0, int& t) {
-    const int d = lane + 64 * i;
-    int k;
-    if (i < 7) k = rt0 + 2 * d;
-    else if (i == 7) k = d < 493 ? rt0 + 2 * d : 1240 + 2 * (d - 493);
-    else {
-        if (d >= kItemsC) { t = 0; return -1; }
-        k = 1240 + 2 * (d - 493);
-    }
-    if (i == 0 && k < 48) { t = 1832 + k; return 0; }   // rt < 48 only (rx_timing 3 before a first valid frame)
-    if (i < 7 || (i == 7 && d < 493)) { t = k - 48; return 1; }
-    if (k < 1288) { t = 1832 + (k - 1240); return 1; }
-    t = k - 1288;
-    return 2;
-}
-template <int i>
-__device__ __forceinline__ void load_item_c(const Src& s, int lane, int rt0, int& r) {
-    int t;
-    const int f = item_c<i>(lane, rt0, t);
-    if (f >= 0) r = *reinterpret_cast<const int*>((f == 0 ? s.xm2 : f == 1 ? s.xm1 : s.x0) + t);
-}
-template <int... I>
-__device__ __forceinline__ void prefetch_c_seq(const Src& s, int lane, int rt0, int (&r)[kPfC],
-                                               std::integer_sequence<int, I...>) {
-    (load_item_c<I>(s, lane, rt0, r[I]), ...);
-}
-[[maybe_unused]] __device__ __forceinline__ void prefetch_c(const Src& s, int lane, int rt0, int (&r)[kPfC]) {
-    prefetch_c_seq(s, lane, rt0, r, std::make_integer_sequence<int, kPfC>{});
-}
-// mix_item on the compact item map, frame g-1 negated when NO
-template <int i, bool NO>
-__device__ __forceinline__ void mix_item_c(int lane, int rt0, int r, const float2* P, float2* M) {
-    int t;
-    const int f = item_c<i>(lane, rt0, t);
-    if (f < 0) return;
-    const float4 p = *reinterpret_cast<const float4*>(P + t);
-    const float v0 = (float)(int16_t)(r & 0xffff);
-    const float v1 = (float)(int16_t)(r >> 16);
-    float4 o;
-    if (i >= 1 && i <= 7) {   // every lane's item is from frame g-1 (item 7's head part too)
-        o = NO ? make_float4((-p.x) * v0, (-p.y) * v0, (-p.z) * v1, (-p.w) * v1)
-               : make_float4(p.x * v0, p.y * v0, p.z * v1, p.w * v1);
-    } else {
-        const float sg = ((f == 1) == NO) ? -1.0f : 1.0f;   // exact sign flip
-        o = make_float4((sg * p.x) * v0, (sg * p.y) * v0, (sg * p.z) * v1, (sg * p.w) * v1);
-    }
-    *reinterpret_cast<float4*>(M + 2 * (lane + 64 * i)) = o;
-}
-template <bool NO, int... I>
-__device__ __forceinline__ void mix_c_seq(int lane, int rt0, const int (&r)[kPfC], const float2* P,
-                                          float2* M, std::integer_sequence<int, I...>) {
-    (mix_item_c<I, NO>(lane, rt0, r[I], P, M), ...);
-}
-[[maybe_unused]] __device__ __forceinline__ void mix_c(int lane, int rt0, const int (&r)[kPfC], unsigned g,
-                                      const float2* P, float2* M) {
-    constexpr auto kSeq = std::make_integer_sequence<int, kPfC>{};
-    if (((g - 1u) & 1u) != 0) mix_c_seq<true>(lane, rt0, r, P, M, kSeq);   // frame g-1 odd
-    else mix_c_seq<false>(lane, rt0, r, P, M, kSeq);
 }
 
 using qhunt::wave_max_u32;
@@ -683,10 +600,9 @@ __device__ __forceinline__ int hunt(int lane, float2* M, const float2* dec, cons
 // correlation of dec_{n+1} = [D_n, F_{n+1}] and its argmax mi.
 // HP (QPSK_HEADPASS): F_{n+1} comes from the head pre-pass (head_kernel), at
 // `head` (global, 51 x 16 B), instead of the head FIR.
-// hoff: where M holds the head's 152 samples (kM1; the compact layout: kHc).
 template <int MODE, bool HP = false>
 __device__ __forceinline__ int front_channel(int lane, int rt, float2* M, float2* dec,
-                                             const float* BT, const float2* head, int hoff FACC_PARAM) {
+                                             const float* BT, const float2* head FACC_PARAM) {
 #ifdef QPSK_STAMPS
     unsigned long long ft0 = stamp_now();
 #endif
@@ -702,7 +618,7 @@ __device__ __forceinline__ int front_channel(int lane, int rt, float2* M, float2
     } else {
         fir_dec(lane, rt, M, dec);
         FSTAMP(0);
-        fir_head_at(lane, M + hoff, dec + QK_NDEC);
+        fir_head_at(lane, M + kM1, dec + QK_NDEC);   // F_{n+1}: M[kM1 ..] (head input)
     }
     wave_lds_sync();
     FSTAMP(1);
@@ -815,9 +731,7 @@ __host__ __device__ constexpr int uix(int i, int j) { return j * (j - 1) / 2 + i
 // EXACT = false: `bmax` collects the bit pattern of the step's largest
 // reciprocal operand xs[4] (the callers test bmax <= bits(2^125) once per
 // frame or job: qk_rcp_in_range() for every step, a NaN or -x has larger bits).
-// RP: the reciprocals' Newton steps on pairs (qk_rcp_pair; the lane back only:
-// in rx_data_kernel ROCm 7.2's greedy register allocator crashes on it)
-template <bool EXACT, bool RP = false>
+template <bool EXACT>
 __device__ __forceinline__ float kal_gain(Kal& k, const f2 (&x)[5], unsigned& bmax) {
     const float E = QK_KAL_E, q = QK_KAL_Q;
     f2 f[5];
@@ -854,16 +768,11 @@ __device__ __forceinline__ float kal_gain(Kal& k, const f2 (&x)[5], unsigned& bm
     } else {
         // the one check: xs[0] >= E unless NaN, and a NaN reaches xs[4] too
         bmax = max(bmax, __float_as_uint(xs[4]));
-        if (RP) {
-            // qk_rcp_fast with the Newton FMAs of two divisors as one packed
-            // FMA each (qk_rcp_pair: the same fmaf per half)
-            qk_rcp_pair(xs[0], xs[1], ys[0], ys[1]);
-            qk_rcp_pair(xs[2], xs[3], ys[2], ys[3]);
-            ys[4] = qk_rcp_fast(xs[4]);
-        } else {
+        // (the Newton steps as packed pairs: 15 fewer instructions per 4
+        // steps but 4 more spilled VGPRs in the 4x2 kernel, C3 +0.8%,
+        // profiles/r05_knobs_ab.txt, code in commit 868e9f0)
 #pragma unroll
-            for (int j = 0; j < 5; j++) ys[j] = qk_rcp_fast(xs[j]);
-        }
+        for (int j = 0; j < 5; j++) ys[j] = qk_rcp_fast(xs[j]);
     }
     float y = ys[0];                                      // 6.19
     k.d[0] = k.d[0] * ((hq * (E + ht)) * y);              // 6.20 (both halves)
@@ -885,9 +794,9 @@ __device__ __forceinline__ float kal_gain(Kal& k, const f2 (&x)[5], unsigned& bm
 
 // update_eq (src/equalizer.c:25-40): the gain, then error *= kalman_y and
 // eq_i += error * conj(g_i)
-template <bool EXACT, bool RP = false>
+template <bool EXACT>
 __device__ __forceinline__ void update_eq(Kal& k, const f2 (&x)[5], f2 e, unsigned& bmax) {
-    const float y = kal_gain<EXACT, RP>(k, x, bmax);
+    const float y = kal_gain<EXACT>(k, x, bmax);
     e = e * y;                                            // error *= kalman_y
 #pragma unroll
     for (int i = 0; i < 5; i++) k.eq[i] = k.eq[i] + cmulc(e, k.g[i]);
@@ -1017,7 +926,7 @@ __device__ __forceinline__ int train(Kal& k, f2 (&x)[5], const f2* wp2, bool& ba
 #pragma unroll
         for (int t = 0; t < 5; t++) v = v + cmul(x[t], k.eq[t]);
         const float er = ref - v.x;                // conjf(ref - val) = (ref - vr, vi)
-        update_eq<EXACT, QPSK_RCP_PAIR != 0>(k, x, f2{er, v.y}, bmax);
+        update_eq<EXACT>(k, x, f2{er, v.y}, bmax);
         if (er * ref > 0.0f) matches++;
 #pragma unroll
         for (int t = 0; t < 4; t++) x[t] = x[t + 1];
@@ -1515,38 +1424,26 @@ __global__ void __launch_bounds__(256) rx_data_kernel(const float4* jobs, unsign
 //
 // QUAD (DUAL, G == 1 only): the back waves hold a quad of lanes per channel
 // (back_frame_quad), 16 channels per wave, W / 16 waves per frame chain.
-//
-// AB (QPSK_FRONT_AB variant builds only, the C3 occupancy A/B of DESIGN.md; 0 in
-// the product): 1 = the 4x2 kernel with the compact front input (item_c) and
-// one dec buffer per front wave; 2 = the same fronts with no back waves at all
-// (timing only: every frame reuses the call's first rx_timing), so that G x FP
-// = 12 fronts fit one CU's VGPRs (3 waves per SIMD at <= 168) and LDS.
-template <int G, int FP, int MODE, bool DUAL, int W, bool QUAD, int AB = 0>
-constexpr int kBackWavesOf = AB == 2 ? 0 : DUAL ? 2 * G * (QUAD ? W / 16 : 1) : G;
+template <int G, int FP, int MODE, bool DUAL, int W, bool QUAD>
+constexpr int kBackWavesOf = DUAL ? 2 * G * (QUAD ? W / 16 : 1) : G;
 
 // waves per SIMD = ceil(waves / 4): 3 (<= 168 VGPRs) for the 12-wave shapes
-template <int G, int FP, int MODE, bool DUAL, int W, bool QUAD, int AB = 0>
-constexpr int kWavesOf = kBackWavesOf<G, FP, MODE, DUAL, W, QUAD, AB> + G * FP;
+template <int G, int FP, int MODE, bool DUAL, int W, bool QUAD>
+constexpr int kWavesOf = kBackWavesOf<G, FP, MODE, DUAL, W, QUAD> + G * FP;
 
 //
 // HP: the fronts take F_{n+1} from the head pre-pass (head_kernel, QPSK_HEADPASS).
-template <int G, int FP, int MODE, bool DUAL, int W = QK_GROUP, bool QUAD = false, bool HP = false,
-          int AB = 0>
-__global__ void __launch_bounds__((64 * kWavesOf<G, FP, MODE, DUAL, W, QUAD, AB>),
-                                  ((kWavesOf<G, FP, MODE, DUAL, W, QUAD, AB> + 3) / 4)) QPSK_RX_ATTR rx_kernel(
+template <int G, int FP, int MODE, bool DUAL, int W = QK_GROUP, bool QUAD = false, bool HP = false>
+__global__ void __launch_bounds__((64 * kWavesOf<G, FP, MODE, DUAL, W, QUAD>),
+                                  ((kWavesOf<G, FP, MODE, DUAL, W, QUAD> + 3) / 4)) QPSK_RX_ATTR rx_kernel(
     const int16_t* in, int16_t* hist, const float2* ptab, const unsigned long long* ks,
     float2* win0, float2* win1, int* mi0, int* mi1, int* rt0, int* rt1, uint8_t* bits,
     uint8_t* valid, int32_t* trace, float2* soft, float4* jobs, unsigned* njobs, int nch, int F,
     unsigned g0, int roles, const float* fft_tab, unsigned long long jcap, int* err) {
     static_assert(W == QK_GROUP || (DUAL && G == 1 && W % FP == 0 && W <= QK_GROUP), "group width");
     static_assert(!QUAD || (DUAL && G == 1 && W % 16 == 0), "quad backs: dual chain, one group");
-    static_assert(AB == 0 || (!DUAL && MODE == 0 && !HP), "front A/B: the 4x2 reference kernel only");
-    constexpr bool kCM = AB != 0;                       // compact front input, one dec buffer
-    // QPSK_COMPACT_NEXT: the 4x2 (non-dual) reference fronts mix the compact input
-    // for every channel but a frame's first
-    constexpr bool kCN = QPSK_COMPACT_NEXT && !DUAL && MODE == 0 && !HP && AB == 0;
     constexpr int kGroups = G, kFrontPer = FP;
-    constexpr int kBackWaves = kBackWavesOf<G, FP, MODE, DUAL, W, QUAD, AB>;
+    constexpr int kBackWaves = kBackWavesOf<G, FP, MODE, DUAL, W, QUAD>;
     constexpr int kChainWaves = QUAD ? W / 16 : 1;     // back waves per frame chain and group
     constexpr bool kDyn = DUAL && (QPSK_DYNPRIO == 2 || (QPSK_DYNPRIO == 1 && QUAD));
     constexpr int kFrontCh = W / kFrontPer;            // channels per front wave
@@ -1558,7 +1455,7 @@ __global__ void __launch_bounds__((64 * kWavesOf<G, FP, MODE, DUAL, W, QUAD, AB>
                    HP ? reinterpret_cast<const float2*>(fft_tab) : nullptr};
     __shared__ __attribute__((aligned(16))) float2 P[QK_FRAME];
     constexpr int DM = MODE & 1;   // decimation semantics; MODE & 2: FFT hunt
-    constexpr int kM = kCM ? kMc : Cfg<DM>::kM, kDecBuf = kCM ? 1 : Cfg<DM>::kDecBuf;
+    constexpr int kM = Cfg<DM>::kM, kDecBuf = Cfg<DM>::kDecBuf;
     __shared__ __attribute__((aligned(16))) float2 Ms[kFrontWaves][kM];
     __shared__ __attribute__((aligned(16))) float2 decs[kFrontWaves][kDecBuf][kDec];
     __shared__ int mi_s[kGroups][2][QK_GROUP], rt_s[kGroups][2][QK_GROUP];
@@ -1590,7 +1487,6 @@ __global__ void __launch_bounds__((64 * kWavesOf<G, FP, MODE, DUAL, W, QUAD, AB>
         if (lane < W && ch < a.nch) {
             mi_s[wave][0][lane] = mi_of(a, a.g0)[ch];
             rt_s[wave][0][lane] = rt_of(a, a.g0)[ch];
-            if (AB == 2) rt_s[wave][1][lane] = rt_s[wave][0][lane];   // no backs: timing only
         }
     }
     if (threadIdx.x < 2 * kGroups * kChainWaves) (&bseq[0][0][0])[threadIdx.x] = (&fcnt[0][0][0])[threadIdx.x] = 0;
@@ -1746,7 +1642,7 @@ __global__ void __launch_bounds__((64 * kWavesOf<G, FP, MODE, DUAL, W, QUAD, AB>
                 wave_lds_sync();                                                                               \
                 STAMP(1);                                                                                      \
                 pmi = front_channel<MODE, HP>(lane, rt_s[gi][p][i0 + c], M, dcur, BT,                          \
-                                              a.heads + ((size_t)ch * a.F + n) * kHeadOut, kM1 FACC_ARG);      \
+                                              a.heads + ((size_t)ch * a.F + n) * kHeadOut FACC_ARG);           \
                 if (lane == 0) mi_s[gi][p ^ 1][i0 + c] = pmi;                                                  \
                 if (c + 1 == nl) store_window(lane, pmi, dcur, wout + (size_t)ch * kWinStride);                \
                 wave_lds_sync();                                                                               \
@@ -1825,44 +1721,6 @@ __global__ void __launch_bounds__((64 * kWavesOf<G, FP, MODE, DUAL, W, QUAD, AB>
         float2* M = Ms[f];
         const bool on = (a.roles & 2) != 0 && nlive > 0;
         if (((a.roles >> 4) & 3) == 1) __builtin_amdgcn_s_setprio(2);
-        if constexpr (kCM) {
-            // the 4x2 front on the compact input (AB variants): a channel's
-            // prefetch needs its rx_timing, so the frame's first channel is
-            // fetched after the frame barrier; one dec buffer (the previous
-            // channel's window is stored before this channel's FIR rewrites it)
-            float2* dec = decs[f][0];
-            int pf[kPfC];
-            // channels [cb, cb + nl) of the group: 32 + 32 (FP = 2), 21 + 21 + 22 (FP = 3)
-            const int fl = f % kFrontPer;
-            const int cb = QK_GROUP * fl / kFrontPer;
-            const int c0 = (grp0 + gi) * QK_GROUP + cb;
-            const int nl = max(0, min(QK_GROUP * (fl + 1) / kFrontPer - cb, a.nch - c0));
-            const bool act = (a.roles & 2) != 0 && nl > 0;
-            STAMP_DECL
-            for (int n = 0; n < a.F; n++) {
-                const int p = n & 1;
-                const unsigned g = a.g0 + (unsigned)n;
-                float2* wout = win_of(a, g + 1u);
-                int pmi = 0;
-                if (act) prefetch_c(srcs(a, c0, n), lane, rt_s[gi][p][cb] & ~1, pf);
-                for (int c = 0; act && c < nl; c++) {
-                    const int ch = c0 + c;
-                    const int rt = rt_s[gi][p][cb + c], rt0 = rt & ~1;
-                    mix_c(lane, rt0, pf, g, P, M);
-                    if (c > 0) store_window(lane, pmi, dec, wout + (size_t)(ch - 1) * kWinStride);
-                    if (c + 1 < nl) prefetch_c(srcs(a, ch + 1, n), lane, rt_s[gi][p][cb + c + 1] & ~1, pf);
-                    wave_lds_sync();
-                    pmi = front_channel<MODE, false>(lane, rt - rt0, M, dec, BT, nullptr, kHc FACC_ARG);
-                    if (lane == 0) mi_s[gi][p ^ 1][cb + c] = pmi;
-                    if (c + 1 == nl) store_window(lane, pmi, dec, wout + (size_t)ch * kWinStride);
-                    wave_lds_sync();
-                }
-                __syncthreads();
-            }
-            STAMP_FLUSH();
-            carry_history<DM>(a.in, a.hist, a.F, c0, nl, lane);
-            return;
-        }
         int pf[kPf<DM>];
         if (on) prefetch<DM>(srcs(a, ch0, 0), lane, pf);
         STAMP_DECL
@@ -1880,29 +1738,18 @@ __global__ void __launch_bounds__((64 * kWavesOf<G, FP, MODE, DUAL, W, QUAD, AB>
             for (int c = 0; on && c < nlive; c++) {
                 const int ch = ch0 + c;
                 float2* dcur = decs[f][c % kDecBuf];
-                const int rt = rt_s[gi][p][cbeg + c];
-                // kCN (QPSK_COMPACT_NEXT): channels after the frame's first were
-                // prefetched with their rx_timing known, as the compact input
-                // (item_c: 569 items instead of 696); the first, fetched during
-                // the previous frame (rx_timing not decided yet), is the full one
-                const int rt0 = (kCN && c > 0) ? (rt & ~1) : 0;
-                if (kCN && c > 0) mix_c(lane, rt0, *reinterpret_cast<int(*)[kPfC]>(&pf[0]), g, P, M);
-                else mix<DM>(lane, pf, g, P, M);
+                mix<DM>(lane, pf, g, P, M);
                 STAMP(0);
                 if (c > 0) store_window(lane, pmi, decs[f][(c - 1) % kDecBuf], wout + (size_t)(ch - 1) * kWinStride);
                 {   // next channel of this frame, else the first of the next frame
                     const bool same = c + 1 < nlive;
-                    if (kCN && same)
-                        prefetch_c(srcs(a, ch + 1, n), lane, rt_s[gi][p][cbeg + c + 1] & ~1,
-                                   *reinterpret_cast<int(*)[kPfC]>(&pf[0]));
-                    else if (same || n + 1 < a.F)
+                    if (same || n + 1 < a.F)
                         prefetch<DM>(srcs(a, same ? ch + 1 : ch0, same ? n : n + 1), lane, pf);
                 }
                 wave_lds_sync();
                 STAMP(1);
-                pmi = front_channel<MODE, HP>(lane, rt - rt0, M, dcur, BT,
-                                              a.heads + ((size_t)ch * a.F + n) * kHeadOut,
-                                              (kCN && c > 0) ? kHc : kM1 FACC_ARG);
+                pmi = front_channel<MODE, HP>(lane, rt_s[gi][p][cbeg + c], M, dcur, BT,
+                                              a.heads + ((size_t)ch * a.F + n) * kHeadOut FACC_ARG);
                 if (lane == 0) mi_s[gi][p ^ 1][cbeg + c] = pmi;
                 if (c + 1 == nlive) store_window(lane, pmi, dcur, wout + (size_t)ch * kWinStride);
                 wave_lds_sync();
@@ -2413,23 +2260,6 @@ int qpsk_rx_launch(qpsk_ctx* c, const int16_t* d_in, int F, uint8_t* d_bits, uin
         }                                                                                      \
     } while (0)
 #define QPSK_LAUNCH_MODE(MM) QPSK_LAUNCH_SHAPES(MM, false)
-#ifdef QPSK_FRONT_AB
-    // the C3 occupancy A/B (variant builds only): 1 = 4x2 with the compact
-    // front input, 2 = its 12 fronts alone (timing only, output invalid)
-    if (!hp && c->mode == QPSK_MODE_REFERENCE && sh.kind == Shape::k4x2) {
-        const dim3 grid((unsigned)((c->nch + 4 * QK_GROUP - 1) / (4 * QK_GROUP))), block(64 * 12);
-#define QPSK_LAUNCH_AB(FF, AA)                                                                  \
-        hipLaunchKernelGGL((rx_kernel<4, FF, 0, false, 64, false, false, AA>), grid, block, 0, s, \
-                           d_in, c->d_hist, c->d_ptab, c->d_ks, c->d_win[0], c->d_win[1],      \
-                           c->d_mi[0], c->d_mi[1], c->d_rt[0], c->d_rt[1], d_bits, d_valid,   \
-                           d_trace, reinterpret_cast<float2*>(d_soft), c->d_jobs,             \
-                           c->d_njobs + parity, c->nch, F, (unsigned)(c->frames & 0xffffffffu), \
-                           sh.roles, c->d_fft, (unsigned long long)c->jobs_cap, d_err)
-        if (QPSK_FRONT_AB == 2) QPSK_LAUNCH_AB(3, 2);
-        else QPSK_LAUNCH_AB(2, 1);
-#undef QPSK_LAUNCH_AB
-    } else
-#endif
     if (hp) {   // head pre-pass: every channel-frame's F_{n+1}, then the frame loop
         const size_t ncf = (size_t)c->nch * (size_t)F;
         hipLaunchKernelGGL(head_kernel, dim3((unsigned)((ncf + 3) / 4)), dim3(256), 0, s, d_in,
