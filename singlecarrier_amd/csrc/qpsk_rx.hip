@@ -2387,6 +2387,12 @@ static Stage stage_of(size_t cf) {
 }
 // calls up to this many input bytes stage through pinned memory
 constexpr size_t kPinnedStage = (size_t)8 << 20;
+// calls up to this many channel-frames (the drop-in qpsk_rx_frame: one) run
+// their kernels on the pinned block itself, no copies (QPSK_ZERO_COPY A/B knob)
+#ifndef QPSK_ZERO_COPY
+#define QPSK_ZERO_COPY 64
+#endif
+constexpr size_t kZeroCopyCF = QPSK_ZERO_COPY;
 
 static int stage_grow(qpsk_ctx* c, size_t F) {
     if (F <= c->s_frames) return QPSK_OK;
@@ -2419,6 +2425,29 @@ extern "C" int qpsk_rx_batch(qpsk_ctx* c, const int16_t* in, int F, uint8_t* bit
     char* h = pin ? c->s_pin : nullptr;
     const size_t nin = sizeof(int16_t) * cf * QK_FRAME;
     const size_t ntr = sizeof(int32_t) * cf * 4, nso = sizeof(float) * cf * QK_NDSYM * 2;
+    if (pin && cf <= kZeroCopyCF) {
+        // tiny calls: the kernels read the input from and write the outputs to
+        // the pinned block directly (device-accessible host memory); the
+        // per-frame latency is then two launches and one synchronisation, not
+        // two copies besides (the kernels touch these few KB once)
+        memcpy(h + g.in, in, nin);
+        r = qpsk_rx_batch_device(c, reinterpret_cast<int16_t*>(h + g.in), F,
+                                 reinterpret_cast<uint8_t*>(h + g.bits), reinterpret_cast<uint8_t*>(h + g.valid),
+                                 trace ? reinterpret_cast<int32_t*>(h + g.trace) : nullptr,
+                                 soft ? reinterpret_cast<float*>(h + g.soft) : nullptr, c->stream);
+        if (r != QPSK_OK) return r;
+        hipLaunchKernelGGL(err_take_to_kernel, dim3(1), dim3(64), 0, c->stream, c->d_err,
+                           reinterpret_cast<int*>(h + g.err));
+        HCHECK(hipGetLastError());
+        HCHECK(hipStreamSynchronize(c->stream));
+        memcpy(bits, h + g.bits, cf * QK_NBITS);
+        memcpy(valid, h + g.valid, cf);
+        if (trace) memcpy(trace, h + g.trace, ntr);
+        if (soft) memcpy(soft, h + g.soft, nso);
+        int e;
+        memcpy(&e, h + g.err, sizeof e);
+        return e != 0 ? QPSK_ESTALL : QPSK_OK;
+    }
     if (pin) memcpy(h + g.in, in, nin);
     HCHECK(hipMemcpyAsync(d + g.in, pin ? (const void*)(h + g.in) : (const void*)in, nin,
                           hipMemcpyHostToDevice, c->stream));
