@@ -7,5 +7,5 @@ OUT=$(mktemp /tmp/asmcount.XXXX.s)
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off \
   -fhip-fp32-correctly-rounded-divide-sqrt -fno-gpu-flush-denormals-to-zero -fno-fast-math \
   -I../../include -I. -mllvm -amdgpu-sched-strategy=iterative-ilp "$@" --cuda-device-only -S -o $OUT qpsk_rx.hip
-python3 ../../profiles/loopstat.py $OUT "${KERN:-rx_kernelILi4ELi2ELi0ELb0ELi64ELb0ELb0ELi0E}" | awk '$4 > 800'
+python3 ../../profiles/loopstat.py $OUT "${KERN:-rx_kernelILi4ELi2ELi0ELb0ELi64ELb0ELb0E}" | awk '$4 > 800'
 rm -f $OUT
