@@ -80,6 +80,19 @@ constexpr int kDec = 296;
 #ifndef QPSK_FIR_WAIT
 #define QPSK_FIR_WAIT 1   // the FIRs: one lgkmcnt(0) per sample batch, not one per sample (0: A/B knob)
 #endif
+#ifndef QPSK_FRESH_SPLIT
+#define QPSK_FRESH_SPLIT 1   // QPSK_FRESH of the 4x2 kernel's fronts with the split FIR (A/B knob)
+#endif
+#ifndef QPSK_FIR_SPLIT
+// the 4x2 kernel in reference mode (MODE 0, not the head pre-pass, not the
+// FFT hunt): before the hunt only dec[0..254], the entries it correlates, in
+// two passes on all 64 lanes (392 packed operations instead of 490);
+// dec[255..289] after it, only when the window's observable part reaches them
+// (fir_split below).  The dual-chain shapes keep fir_dec + fir_head_at: their
+// fronts are latency-bound and the split's extra LDS reads cost them ~1%
+// (profiles/r05_split_ab.txt); 0: A/B knob
+#define QPSK_FIR_SPLIT 1
+#endif
 #ifndef QPSK_QDMUL
 #define QPSK_QDMUL 1   // quad step: rotated h times its column mask as v_mul_f32_dpp (qd_mul); 0: A/B knob
 #endif
@@ -297,9 +310,9 @@ __device__ __forceinline__ int fresh_lane(int lane) {
     return lane;
 }
 
-template <int MODE, bool CG = false>
+template <int MODE, bool CG = false, int FR = QPSK_FRESH>
 __device__ __forceinline__ void prefetch(const Src& s, int lane, int (&r)[kPf<MODE>]) {
-    prefetch_seq<MODE, CG>(s, QPSK_FRESH ? fresh_lane(lane) : lane, r, std::make_integer_sequence<int, kPf<MODE>>{});
+    prefetch_seq<MODE, CG>(s, (FR & 1) ? fresh_lane(lane) : lane, r, std::make_integer_sequence<int, kPf<MODE>>{});
 }
 
 // src/qpsk.c:139-144 as (-1)^G * P[t] * (x * 2^-14), two samples per item.
@@ -333,11 +346,11 @@ __device__ __forceinline__ void mix_seq(int lane, const int (&r)[kPf<MODE>], con
     (mix_item<MODE, I, NO>(lane, r[I], P, M), ...);
 }
 
-template <int MODE>
+template <int MODE, int FR = QPSK_FRESH>
 __device__ __forceinline__ void mix(int lane, const int (&r)[kPf<MODE>], unsigned g,
                                     const float2* P, float2* M) {
     constexpr auto kSeq = std::make_integer_sequence<int, kPf<MODE>>{};
-    if (QPSK_FRESH) lane = fresh_lane(lane);
+    if (FR & 2) lane = fresh_lane(lane);
     if (((g - 1u) & 1u) != 0) mix_seq<MODE, true>(lane, r, P, M, kSeq);   // frame g-1 odd
     else mix_seq<MODE, false>(lane, r, P, M, kSeq);
 }
@@ -476,6 +489,94 @@ __device__ __forceinline__ void fir_dec(int lane, int rt, const float2* M, float
     }
 }
 
+// One FIR output per lane: out = GAIN * sum_k b[k] * RRC[k], k ascending
+// (the same operations in the same order as fir_dec / fir_head_at).
+#ifndef QPSK_FB1
+#define QPSK_FB1 8   // fir_one's samples per LDS batch (A/B knob)
+#endif
+__device__ __forceinline__ f2 fir_one(const float2* b) {
+    f2 y = {0.0f, 0.0f};
+#pragma unroll
+    for (int s0 = 0; s0 < QK_NTAPS; s0 += QPSK_FB1) {
+        f2 v[QPSK_FB1];
+#pragma unroll
+        for (int j = 0; j < QPSK_FB1; j++)
+            if (s0 + j < QK_NTAPS) v[j] = ld2nt(b + s0 + j);
+        if (QPSK_FIR_WAIT) {
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int j = 0; j < QPSK_FB1; j++)
+            if (s0 + j < QK_NTAPS) y = y + v[j] * QK_RRC[s0 + j];
+    }
+    return y * QK_GAIN;
+}
+
+// The split FIR of reference mode (QPSK_FIR_SPLIT).  dec = [D_n[0..187],
+// F_{n+1}[0..101]]; the hunt correlates dec[0..254] (lags < 128 over 128
+// symbols) and the window's observable entries are dec[mi .. mi+162]
+// (slots past the data symbols never reach an output), so
+// F_{n+1}[67..101] = dec[255..289] matter only when mi >= 93.  Every output is
+// one 49-tap dot product over consecutive samples, so a lane's outputs may come
+// from D or from F as long as its code is the same:
+//   pass 1 (fir_dec's code: 3 outputs 5 samples apart): lanes 0..62 D[3l ..
+//     3l+2] (D[188] of lane 62 discarded), lane 63 F[56], F[61], F[66];
+//   pass 2 (one output per lane): F[l + (l >= 56) + (l >= 60)], 0..66 less
+//     56, 61, 66;
+//   after the hunt, mi >= 93: F[67 + l], l < 35 (fir_split_tail).
+// 392 packed operations before the hunt (294 + 98) instead of 490, and 98 more
+// for the ~27% of channels whose window reaches past dec[254].
+constexpr int kSplitMi = 255 - (QK_NPRE + QK_NDSYM + 3);   // 93: mi + 162 >= 255
+__device__ __forceinline__ void fir_split(int lane, int rt, const float2* M, float2* dec) {
+    lane = fresh_lane(lane);   // the per-lane bases below are recomputed, not kept live across the loop
+    {   // pass 1
+        const float2* b = lane < 63 ? M + 15 * lane + rt : M + kM1 + 56;
+        f2 y[3] = {{0.0f, 0.0f}, {0.0f, 0.0f}, {0.0f, 0.0f}};
+#pragma unroll
+        for (int s0 = 0; s0 < 59; s0 += QPSK_FB) {
+            f2 v[QPSK_FB];
+#pragma unroll
+            for (int j = 0; j < QPSK_FB; j++)
+                if (s0 + j < 59) v[j] = ld2nt(b + s0 + j);
+            if (QPSK_FIR_WAIT) {
+                __builtin_amdgcn_sched_barrier(0);
+                __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+                __builtin_amdgcn_sched_barrier(0);
+            }
+#pragma unroll
+            for (int j = 0; j < QPSK_FB; j++) {
+                const int s = s0 + j;
+#pragma unroll
+                for (int m = 0; m < 3; m++) {
+                    const int k = s - 5 * m;
+                    if (s < 59 && k >= 0 && k < QK_NTAPS) y[m] = y[m] + v[j] * QK_RRC[k];
+                }
+            }
+        }
+#pragma unroll
+        for (int m = 0; m < 3; m++) {
+            const f2 o = y[m] * QK_GAIN;
+            const int d = lane < 63 ? 3 * lane + m : QK_NDEC + 56 + 5 * m;
+            if (d < QK_NDEC || lane == 63) dec[d] = make_float2(o.x, o.y);
+        }
+    }
+    {   // pass 2
+        const int j = lane + (lane >= 56 ? 1 : 0) + (lane >= 60 ? 1 : 0);
+        const f2 o = fir_one(M + kM1 + j);
+        dec[QK_NDEC + j] = make_float2(o.x, o.y);
+    }
+}
+
+__device__ __forceinline__ void fir_split_tail(int lane, const float2* M, float2* dec) {
+    lane = fresh_lane(lane);
+    if (lane < QK_NHEAD - 67) {
+        const f2 o = fir_one(M + kM1 + 67 + lane);
+        dec[QK_NDEC + 67 + lane] = make_float2(o.x, o.y);
+    }
+}
+
 // Undecimated head F_{n+1}[j] = fir_out'[j], j < 102: lane l makes j = 2l, 2l+1
 // from M[kM1 + 2l + s], s < 50, read as 16-B sample pairs (lane stride 16 B:
 // ds_read_b128's lane groups cover the 64 banks once; a b64 read at that
@@ -600,7 +701,7 @@ __device__ __forceinline__ int hunt(int lane, float2* M, const float2* dec, cons
 // correlation of dec_{n+1} = [D_n, F_{n+1}] and its argmax mi.
 // HP (QPSK_HEADPASS): F_{n+1} comes from the head pre-pass (head_kernel), at
 // `head` (global, 51 x 16 B), instead of the head FIR.
-template <int MODE, bool HP = false>
+template <int MODE, bool HP = false, bool SPLIT = false>
 __device__ __forceinline__ int front_channel(int lane, int rt, float2* M, float2* dec,
                                              const float* BT, const float2* head FACC_PARAM) {
 #ifdef QPSK_STAMPS
@@ -615,6 +716,17 @@ __device__ __forceinline__ int front_channel(int lane, int rt, float2* M, float2
         fir_dec(lane, rt, M, dec);
         FSTAMP(0);
         if (lane < kHeadOut / 2) *reinterpret_cast<float4*>(dec + QK_NDEC + 2 * lane) = h;
+    } else if constexpr (MODE == 0 && SPLIT) {
+        fir_split(lane, rt, M, dec);   // dec[0..254]
+        FSTAMP(0);
+        wave_lds_sync();
+        FSTAMP(1);
+        const int mi = hunt<MODE>(lane, M, dec, BT FACC_FWD);
+        if (mi >= kSplitMi) {          // wave-uniform
+            fir_split_tail(lane, M, dec);   // dec[255..289]
+            wave_lds_sync();
+        }
+        return mi;
     } else {
         fir_dec(lane, rt, M, dec);
         FSTAMP(0);
@@ -1713,6 +1825,10 @@ __global__ void __launch_bounds__((64 * kWavesOf<G, FP, MODE, DUAL, W, QUAD>),
         // ------------------------------------------------------------ front
         // channel by channel: mix (prefetched samples) -> store the previous
         // channel's window -> prefetch the next channel -> FIR/correlate/argmax
+        // the split FIR (fir_split) and, to keep the channel loop's per-lane
+        // constants out of scratch beside it, recomputed prefetch offsets
+        constexpr bool kSplit = MODE == 0 && !HP && QPSK_FIR_SPLIT;
+        constexpr int kFr = kSplit ? QPSK_FRESH_SPLIT : QPSK_FRESH;
         const int f = wave - kBackWaves;
         const int gi = f / kFrontPer;
         const int cbeg = (f % kFrontPer) * kFrontCh;
@@ -1722,7 +1838,7 @@ __global__ void __launch_bounds__((64 * kWavesOf<G, FP, MODE, DUAL, W, QUAD>),
         const bool on = (a.roles & 2) != 0 && nlive > 0;
         if (((a.roles >> 4) & 3) == 1) __builtin_amdgcn_s_setprio(2);
         int pf[kPf<DM>];
-        if (on) prefetch<DM>(srcs(a, ch0, 0), lane, pf);
+        if (on) prefetch<DM, false, kFr>(srcs(a, ch0, 0), lane, pf);
         STAMP_DECL
         for (int n = 0; n < a.F; n++) {
             const int p = n & 1;
@@ -1738,17 +1854,17 @@ __global__ void __launch_bounds__((64 * kWavesOf<G, FP, MODE, DUAL, W, QUAD>),
             for (int c = 0; on && c < nlive; c++) {
                 const int ch = ch0 + c;
                 float2* dcur = decs[f][c % kDecBuf];
-                mix<DM>(lane, pf, g, P, M);
+                mix<DM, kFr>(lane, pf, g, P, M);
                 STAMP(0);
                 if (c > 0) store_window(lane, pmi, decs[f][(c - 1) % kDecBuf], wout + (size_t)(ch - 1) * kWinStride);
                 {   // next channel of this frame, else the first of the next frame
                     const bool same = c + 1 < nlive;
                     if (same || n + 1 < a.F)
-                        prefetch<DM>(srcs(a, same ? ch + 1 : ch0, same ? n : n + 1), lane, pf);
+                        prefetch<DM, false, kFr>(srcs(a, same ? ch + 1 : ch0, same ? n : n + 1), lane, pf);
                 }
                 wave_lds_sync();
                 STAMP(1);
-                pmi = front_channel<MODE, HP>(lane, rt_s[gi][p][cbeg + c], M, dcur, BT,
+                pmi = front_channel<MODE, HP, kSplit>(lane, rt_s[gi][p][cbeg + c], M, dcur, BT,
                                               a.heads + ((size_t)ch * a.F + n) * kHeadOut FACC_ARG);
                 if (lane == 0) mi_s[gi][p ^ 1][cbeg + c] = pmi;
                 if (c + 1 == nlive) store_window(lane, pmi, dcur, wout + (size_t)ch * kWinStride);
