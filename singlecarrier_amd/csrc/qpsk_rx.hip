@@ -90,7 +90,7 @@ constexpr int kDec = 296;
 // dec[255..289] after it, only when the window's observable part reaches them
 // (fir_split below).  The dual-chain shapes keep fir_dec + fir_head_at: their
 // fronts are latency-bound and the split's extra LDS reads cost them ~1%
-// (profiles/r05_split_ab.txt); 0: A/B knob
+// (profiles/r05_split_ab.txt); 0: A/B knob; 2: every MODE-0 shape (A/B knob)
 #define QPSK_FIR_SPLIT 1
 #endif
 #ifndef QPSK_QDMUL
@@ -1708,9 +1708,12 @@ __global__ void __launch_bounds__((64 * kWavesOf<G, FP, MODE, DUAL, W, QUAD>),
             auto blive = [&](int bb) { return max(0, min(mych, a.nch - bch0(bb))); };
             float2* M = Ms[f];
             int pf[kPf<DM>];
+            // QPSK_FIR_SPLIT == 2 (A/B knob): the split FIR here too
+            constexpr bool kSplitD = MODE == 0 && !HP && QPSK_FIR_SPLIT == 2;
+            constexpr int kFrD = kSplitD ? QPSK_FRESH_SPLIT : QPSK_FRESH;
             if (kDyn) __builtin_amdgcn_s_setprio(1);
             else if (((a.roles >> 4) & 3) == 1) __builtin_amdgcn_s_setprio(2);
-            if (blive(0) > 0) prefetch<DM>(srcs(a, bch0(0), 0), lane, pf);
+            if (blive(0) > 0) prefetch<DM, false, kFrD>(srcs(a, bch0(0), 0), lane, pf);
             // diagnostic stamps (QPSK_STAMPS): 7 wait for the backs, 0 mix,
             // 4 window store, 1 prefetch, 8-12 front_channel phases, 6 its tail,
             // 5 signal
@@ -1736,7 +1739,7 @@ __global__ void __launch_bounds__((64 * kWavesOf<G, FP, MODE, DUAL, W, QUAD>),
             for (int c = 0; c < nl; c++, k++) {                                                                \
                 const int ch = c0 + c;                                                                         \
                 float2* dcur = decs[f][k % kDecBuf];                                                           \
-                mix<DM>(lane, pf, g, P, M);                                                                    \
+                mix<DM, kFrD>(lane, pf, g, P, M);                                                              \
                 STAMP(0);                                                                                      \
                 if (c > 0)                                                                                     \
                     store_window(lane, pmi, decs[f][(k - 1) % kDecBuf], wout + (size_t)(ch - 1) * kWinStride); \
@@ -1749,11 +1752,11 @@ __global__ void __launch_bounds__((64 * kWavesOf<G, FP, MODE, DUAL, W, QUAD>),
                         while (nb < kChainWaves && blive(nb) == 0) nb++;                                       \
                         if (nb == kChainWaves) { nb = 0; nn = n + 1; }                                         \
                     }                                                                                          \
-                    if (nn < a.F) prefetch<DM, CG>(srcs(a, bch0(nb) + nc, nn), lane, pf);                      \
+                    if (nn < a.F) prefetch<DM, CG, kFrD>(srcs(a, bch0(nb) + nc, nn), lane, pf);                \
                 }                                                                                              \
                 wave_lds_sync();                                                                               \
                 STAMP(1);                                                                                      \
-                pmi = front_channel<MODE, HP>(lane, rt_s[gi][p][i0 + c], M, dcur, BT,                          \
+                pmi = front_channel<MODE, HP, kSplitD>(lane, rt_s[gi][p][i0 + c], M, dcur, BT,                 \
                                               a.heads + ((size_t)ch * a.F + n) * kHeadOut FACC_ARG);           \
                 if (lane == 0) mi_s[gi][p ^ 1][i0 + c] = pmi;                                                  \
                 if (c + 1 == nl) store_window(lane, pmi, dcur, wout + (size_t)ch * kWinStride);                \
