@@ -80,11 +80,6 @@ constexpr int kDec = 296;
 #ifndef QPSK_FIR_WAIT
 #define QPSK_FIR_WAIT 1   // the FIRs: one lgkmcnt(0) per sample batch, not one per sample (0: A/B knob)
 #endif
-#ifndef QPSK_FRONT_DYN
-// 4x2 kernel: the front waves take the block's channels from an LDS counter per
-// frame instead of 32 fixed ones each (1), or the fixed split (0)
-#define QPSK_FRONT_DYN 0
-#endif
 #ifndef QPSK_FRESH_SPLIT
 #define QPSK_FRESH_SPLIT 1   // QPSK_FRESH of the 4x2 kernel's fronts with the split FIR (A/B knob)
 #endif
@@ -1583,7 +1578,6 @@ __global__ void __launch_bounds__((64 * kWavesOf<G, FP, MODE, DUAL, W, QUAD>),
     __shared__ int bseq[kGroups][2][kChainWaves], fcnt[kGroups][2][kChainWaves];
     __shared__ int dead_s;                               // DUAL: a wait of this workgroup timed out
     __shared__ int nwait_s;                              // kDyn: back waves waiting for their fronts
-    __shared__ int claim_s[3];                           // QPSK_FRONT_DYN: channels taken of frame n, [n % 3]
     const int lane = threadIdx.x & 63;
     // wave-uniform by construction; readfirstlane tells the compiler, so every
     // per-wave index and pointer below lives in SGPRs
@@ -1608,7 +1602,7 @@ __global__ void __launch_bounds__((64 * kWavesOf<G, FP, MODE, DUAL, W, QUAD>),
         }
     }
     if (threadIdx.x < 2 * kGroups * kChainWaves) (&bseq[0][0][0])[threadIdx.x] = (&fcnt[0][0][0])[threadIdx.x] = 0;
-    if (threadIdx.x == 0) dead_s = nwait_s = claim_s[0] = claim_s[1] = claim_s[2] = 0;
+    if (threadIdx.x == 0) dead_s = nwait_s = 0;
     __syncthreads();
     if constexpr (DUAL) {
         // Channel blocks: a group's channels split into one block per back wave
@@ -1812,9 +1806,6 @@ __global__ void __launch_bounds__((64 * kWavesOf<G, FP, MODE, DUAL, W, QUAD>),
         STAMP_DECL
         for (int n = 0; n < a.F; n++) {
             const int p = n & 1;
-            // QPSK_FRONT_DYN: frame n+2's counter (frame n-1's, whose claims
-            // ended with the last barrier; frame n+2's start after the next one)
-            if (QPSK_FRONT_DYN && wave == 0 && lane == 0) claim_s[(n + 2) % 3] = 0;
             if (any && (a.roles & 1)) {
                 const int rt = rt_s[gi][p][lane];
                 back_frame(a, live ? ch : 0, live, n, mi_s[gi][p][lane], [=] { return rt; },
@@ -1850,73 +1841,6 @@ __global__ void __launch_bounds__((64 * kWavesOf<G, FP, MODE, DUAL, W, QUAD>),
         const bool on = (a.roles & 2) != 0 && nlive > 0;
         if (((a.roles >> 4) & 3) == 1) __builtin_amdgcn_s_setprio(2);
         int pf[kPf<DM>];
-        if constexpr (QPSK_FRONT_DYN) {
-            // Channels from LDS counters (claim_s[n % 3] for frame n): a wave takes
-            // the block's next channel when it prefetches, so the waves of a SIMD
-            // pair end a frame together instead of the younger one finishing its
-            // fixed 32 alone.  A claim is (frame << 16 | channel of the block), or
-            // -1; in iteration n only frames n and n + 1 are claimed, at most one
-            // of frame n + 1 per wave (the next channel's prefetch).
-            const int chb = grp0 * QK_GROUP;
-            const int nblk = max(0, min(kGroups * QK_GROUP, a.nch - chb));
-            const bool don = (a.roles & 2) != 0 && nblk > 0;
-            auto claim = [&](int f0, int f1) {
-                for (int fr = f0; fr <= f1 && fr < a.F; fr++) {
-                    int idx = 0;
-                    if (lane == 0)
-                        idx = __hip_atomic_fetch_add(&claim_s[fr % 3], 1, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_WORKGROUP);
-                    idx = __builtin_amdgcn_readfirstlane(idx);
-                    if (idx < nblk) return (fr << 16) | idx;
-                }
-                return -1;
-            };
-            int cur = don ? claim(0, 0) : -1;
-            if (cur >= 0) prefetch<DM, false, kFr>(srcs(a, chb + (cur & 0xffff), cur >> 16), lane, pf);
-            int k = 0;   // channels done, for the dec buffer ring
-            STAMP_DECL
-            for (int n = 0; n < a.F; n++) {
-                const int p = n & 1;
-                const unsigned g = a.g0 + (unsigned)n;
-                float2* wout = win_of(a, g + 1u);
-                if (don && cur < 0) {   // nothing held (a block of < 8 channels)
-                    cur = claim(n, n + 1);
-                    if (cur >= 0) prefetch<DM, false, kFr>(srcs(a, chb + (cur & 0xffff), cur >> 16), lane, pf);
-                }
-                int prev = -1, pmi = 0;   // the previous channel of this frame, its window not stored yet
-                while (cur >= 0 && (cur >> 16) == n) {
-                    const int ci = cur & 0xffff, gc = ci / QK_GROUP, li = ci % QK_GROUP;
-                    const int ch = chb + ci;
-                    float2* dcur = decs[f][k % kDecBuf];
-                    mix<DM, kFr>(lane, pf, g, P, M);
-                    STAMP(0);
-                    if (prev >= 0)
-                        store_window(lane, pmi, decs[f][(k - 1) % kDecBuf], wout + (size_t)(chb + prev) * kWinStride);
-                    const int nxt = claim(n, n + 1);
-                    if (nxt >= 0) prefetch<DM, false, kFr>(srcs(a, chb + (nxt & 0xffff), nxt >> 16), lane, pf);
-                    wave_lds_sync();
-                    STAMP(1);
-                    pmi = front_channel<MODE, HP, kSplit>(lane, rt_s[gc][p][li], M, dcur, BT,
-                                                          a.heads + ((size_t)ch * a.F + n) * kHeadOut FACC_ARG);
-                    if (lane == 0) mi_s[gc][p ^ 1][li] = pmi;
-                    if (nxt < 0 || (nxt >> 16) != n) {
-                        store_window(lane, pmi, dcur, wout + (size_t)ch * kWinStride);
-                        prev = -1;
-                    } else {
-                        prev = ci;
-                    }
-                    wave_lds_sync();
-                    STAMP(6);
-                    cur = nxt;
-                    k++;
-                }
-                __syncthreads();
-                STAMP(7);
-            }
-            STAMP_FLUSH();
-            carry_history<DM>(a.in, a.hist, a.F, ch0, nlive, lane);
-            return;
-        }
         if (on) prefetch<DM, false, kFr>(srcs(a, ch0, 0), lane, pf);
         STAMP_DECL
         for (int n = 0; n < a.F; n++) {
