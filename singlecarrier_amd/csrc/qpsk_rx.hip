@@ -1483,7 +1483,11 @@ __global__ void __launch_bounds__(256) rx_data_kernel(const float4* jobs, unsign
                                                       unsigned* njobs,
                                                       const unsigned long long* ks_tab,
                                                       uint8_t* bits, float2* soft, int parity,
-                                                      int force_exact) {
+                                                      int force_exact, int* err, int* err_to) {
+    // err_to (host calls, qpsk_rx_batch): the context's error word, taken in one
+    // atomic exchange after rx_kernel (stream order), stored with the outputs:
+    // no separate launch for it
+    if (err_to && blockIdx.x == 0 && threadIdx.x == 0) *err_to = atomicExch(err, 0);
     const size_t cap = (size_t)jcap;
     const unsigned n = njobs[parity];
     const unsigned stride = gridDim.x * blockDim.x;
@@ -2310,7 +2314,7 @@ static Shape pick_shape(const qpsk_ctx* c) {
 // or a caller's own (qpsk_stream.hip: one per stream slot, so a stall is
 // reported with the chunk it belongs to).
 int qpsk_rx_launch(qpsk_ctx* c, const int16_t* d_in, int F, uint8_t* d_bits, uint8_t* d_valid,
-                   int32_t* d_trace, float* d_soft, hipStream_t s, int* d_err) {
+                   int32_t* d_trace, float* d_soft, hipStream_t s, int* d_err, int* err_to) {
     if (!c || F < 0 || (F > 0 && (!d_in || !d_bits || !d_valid))) return QPSK_EINVAL;
     if (F == 0) return QPSK_OK;
     if ((reinterpret_cast<uintptr_t>(d_in) & 15u) != 0) return QPSK_EINVAL;  // int4 loads
@@ -2403,7 +2407,8 @@ int qpsk_rx_launch(qpsk_ctx* c, const int16_t* d_in, int F, uint8_t* d_bits, uin
     const unsigned dgrid = (unsigned)std::min<size_t>(kDataGrid, (need + kDataBlock - 1) / kDataBlock);
     hipLaunchKernelGGL(rx_data_kernel, dim3(dgrid), dim3(kDataBlock), 0, s, c->d_jobs,
                        (unsigned long long)c->jobs_cap, c->d_njobs, c->d_ks, d_bits,
-                       reinterpret_cast<float2*>(d_soft), parity, c->roles & kForceExact);
+                       reinterpret_cast<float2*>(d_soft), parity, c->roles & kForceExact, c->d_err,
+                       err_to);
     HCHECK(hipGetLastError());
     if (slot >= 0) HCHECK(hipEventRecord(c->ev[slot][2], s));
     HCHECK(hipEventRecord(c->done, s));
@@ -2418,7 +2423,7 @@ extern "C" int qpsk_rx_batch_device(qpsk_ctx* c, const int16_t* d_in, int F, uin
                                     uint8_t* d_valid, int32_t* d_trace, float* d_soft,
                                     void* stream) {
     return qpsk_rx_launch(c, d_in, F, d_bits, d_valid, d_trace, d_soft, (hipStream_t)stream,
-                          nullptr);
+                          nullptr, nullptr);
 }
 
 namespace {
@@ -2426,11 +2431,6 @@ namespace {
 // kernel between a read and a separate clear cannot be lost
 __global__ void err_take_kernel(int* err) {
     if (threadIdx.x == 0) err[1] = atomicExch(&err[0], 0);
-}
-// the same, the taken value stored at `to` (qpsk_rx_batch: inside the staging
-// block, so it comes back with the bits in one copy)
-__global__ void err_take_to_kernel(int* err, int* to) {
-    if (threadIdx.x == 0) *to = atomicExch(&err[0], 0);
 }
 }  // namespace
 
@@ -2550,14 +2550,13 @@ extern "C" int qpsk_rx_batch(qpsk_ctx* c, const int16_t* in, int F, uint8_t* bit
         // per-frame latency is then two launches and one synchronisation, not
         // two copies besides (the kernels touch these few KB once)
         memcpy(h + g.in, in, nin);
-        r = qpsk_rx_batch_device(c, reinterpret_cast<int16_t*>(h + g.in), F,
-                                 reinterpret_cast<uint8_t*>(h + g.bits), reinterpret_cast<uint8_t*>(h + g.valid),
-                                 trace ? reinterpret_cast<int32_t*>(h + g.trace) : nullptr,
-                                 soft ? reinterpret_cast<float*>(h + g.soft) : nullptr, c->stream);
-        if (r != QPSK_OK) return r;
-        hipLaunchKernelGGL(err_take_to_kernel, dim3(1), dim3(64), 0, c->stream, c->d_err,
+        // the error word comes back with the outputs (rx_data_kernel's err_to)
+        r = qpsk_rx_launch(c, reinterpret_cast<int16_t*>(h + g.in), F,
+                           reinterpret_cast<uint8_t*>(h + g.bits), reinterpret_cast<uint8_t*>(h + g.valid),
+                           trace ? reinterpret_cast<int32_t*>(h + g.trace) : nullptr,
+                           soft ? reinterpret_cast<float*>(h + g.soft) : nullptr, c->stream, nullptr,
                            reinterpret_cast<int*>(h + g.err));
-        HCHECK(hipGetLastError());
+        if (r != QPSK_OK) return r;
         HCHECK(hipStreamSynchronize(c->stream));
         memcpy(bits, h + g.bits, cf * QK_NBITS);
         memcpy(valid, h + g.valid, cf);
@@ -2570,10 +2569,14 @@ extern "C" int qpsk_rx_batch(qpsk_ctx* c, const int16_t* in, int F, uint8_t* bit
     if (pin) memcpy(h + g.in, in, nin);
     HCHECK(hipMemcpyAsync(d + g.in, pin ? (const void*)(h + g.in) : (const void*)in, nin,
                           hipMemcpyHostToDevice, c->stream));
-    r = qpsk_rx_batch_device(c, reinterpret_cast<int16_t*>(d + g.in), F,
-                             reinterpret_cast<uint8_t*>(d + g.bits), reinterpret_cast<uint8_t*>(d + g.valid),
-                             trace ? reinterpret_cast<int32_t*>(d + g.trace) : nullptr,
-                             soft ? reinterpret_cast<float*>(d + g.soft) : nullptr, c->stream);
+    // pinned: the error word is taken by rx_data_kernel (err_to) into the
+    // staging block right after the valid flags, so bits, flags and error word
+    // come back in one copy; pageable: qpsk_rx_sync() takes it
+    r = qpsk_rx_launch(c, reinterpret_cast<int16_t*>(d + g.in), F,
+                       reinterpret_cast<uint8_t*>(d + g.bits), reinterpret_cast<uint8_t*>(d + g.valid),
+                       trace ? reinterpret_cast<int32_t*>(d + g.trace) : nullptr,
+                       soft ? reinterpret_cast<float*>(d + g.soft) : nullptr, c->stream, nullptr,
+                       pin ? reinterpret_cast<int*>(d + g.err) : nullptr);
     if (r != QPSK_OK) return r;
     if (!pin) {
         HCHECK(hipMemcpyAsync(bits, d + g.bits, cf * QK_NBITS, hipMemcpyDeviceToHost, c->stream));
@@ -2582,15 +2585,10 @@ extern "C" int qpsk_rx_batch(qpsk_ctx* c, const int16_t* in, int F, uint8_t* bit
         if (soft) HCHECK(hipMemcpyAsync(soft, d + g.soft, nso, hipMemcpyDeviceToHost, c->stream));
         return qpsk_rx_sync(c);
     }
-    // the error word, taken in one atomic exchange behind this call's kernels
-    // (as qpsk_rx_sync: a stream on this context, qpsk_stream_ctx, ORs its
+    // (the error word was taken in one atomic exchange behind rx_kernel, as
+    // qpsk_rx_sync does: a stream on this context, qpsk_stream_ctx, ORs its
     // slots' stalls into the same word from another HIP stream, and a read
-    // followed by a separate clear could lose one merged in between), into the
-    // staging block right after the valid flags: bits, flags and error word
-    // come back in one copy
-    hipLaunchKernelGGL(err_take_to_kernel, dim3(1), dim3(64), 0, c->stream, c->d_err,
-                       reinterpret_cast<int*>(d + g.err));
-    HCHECK(hipGetLastError());
+    // followed by a separate clear could lose one merged in between)
     HCHECK(hipMemcpyAsync(h + g.bits, d + g.bits, g.err + sizeof(int) - g.bits, hipMemcpyDeviceToHost, c->stream));
     if (trace) HCHECK(hipMemcpyAsync(h + g.trace, d + g.trace, ntr, hipMemcpyDeviceToHost, c->stream));
     if (soft) HCHECK(hipMemcpyAsync(h + g.soft, d + g.soft, nso, hipMemcpyDeviceToHost, c->stream));

@@ -10,8 +10,10 @@
 // report stalls to (nullptr: the context's own, which qpsk_rx_sync() takes).
 // qpsk_stream.hip gives each stream slot its own word, so a stall is reported
 // by qpsk_stream_retrieve() for the chunk it happened in.
+// err_to (nullable): where rx_data_kernel stores the context's error word,
+// taken in one atomic exchange once rx_kernel is done (host calls).
 int qpsk_rx_launch(qpsk_ctx* c, const int16_t* d_in, int F, uint8_t* d_bits, uint8_t* d_valid,
-                   int32_t* d_trace, float* d_soft, hipStream_t s, int* d_err);
+                   int32_t* d_trace, float* d_soft, hipStream_t s, int* d_err, int* err_to = nullptr);
 
 // The context's own device error word (qpsk_rx_sync() takes it): a stream
 // slot's stall is OR-ed into it too, so the context sees every stall.
