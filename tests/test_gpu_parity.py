@@ -358,6 +358,23 @@ def test_progress_wait_timeout_is_an_error(monkeypatch):
     _vs_oracle(x)
 
 
+def test_progress_wait_timeout_is_an_error_tiny_call(monkeypatch):
+    """The same for a host call of <= 64 channel-frames (8 channels x 4 frames),
+    which runs on the pinned staging block and gets the error word from
+    rx_data_kernel (no separate launch): the stall still comes back as
+    QPSK_ESTALL, and the word is cleared by being taken."""
+    x = oracle.synth(67, 8, 4, 4.0)
+    monkeypatch.setenv("QPSK_DEBUG_STALL", "1")
+    rx = sc.Receiver(8)
+    with pytest.raises(sc.QpskError) as ei:
+        rx.demod(x)
+    assert ei.value.code == sc.QPSK_ESTALL
+    assert sc.lib().qpsk_rx_sync(rx._h) == 0   # taken by the call
+    rx.close()
+    monkeypatch.delenv("QPSK_DEBUG_STALL")
+    _vs_oracle(x)
+
+
 def test_exact_division_fallback(monkeypatch):
     """The Kalman step's fast reciprocal has an exact-division fallback that
     recomputes a whole frame (rx_kernel) or job (rx_data_kernel) when an
