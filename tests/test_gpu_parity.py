@@ -248,6 +248,19 @@ def test_every_workgroup_shape(shape, monkeypatch):
     _vs_oracle(x)
 
 
+def test_split_fir_window_boundary(monkeypatch):
+    """The 4x2 kernel's split FIR computes dec[255..289] (F_{n+1}[67..101])
+    only after the hunt and only when mi >= 93, where the window's observable
+    part (dec[mi .. mi+162]) reaches them.  On a forced 4x2 batch every output
+    must be exact, and the batch must hold valid frames on both sides of the
+    boundary, the data symbols of the mi >= 93 ones read from the late pass."""
+    monkeypatch.setenv("QPSK_SHAPE", "4x2")
+    x = oracle.synth(71, 512, 8, 8.0)
+    out = _vs_oracle(x)
+    mi = out["trace"][..., 0][out["valid"].astype(bool)]
+    assert (mi >= 93).sum() > 20 and ((mi < 93) & (mi >= 80)).sum() > 5, np.bincount(mi)
+
+
 @pytest.mark.parametrize("width", ["16", "32", "64"])
 def test_dual_chain_group_widths(width, monkeypatch):
     """One group per workgroup runs the dual-chain kernel (back waves for the
