@@ -1571,8 +1571,7 @@ __global__ void __launch_bounds__((64 * kWavesOf<G, FP, MODE, DUAL, W, QUAD>),
                    HP ? reinterpret_cast<const float2*>(fft_tab) : nullptr};
     __shared__ __attribute__((aligned(16))) float2 P[QK_FRAME];
     constexpr int DM = MODE & 1;   // decimation semantics; MODE & 2: FFT hunt
-    // more than 8 front waves (1x10): one dec buffer each, as MODE 1's (LDS)
-    constexpr int kM = Cfg<DM>::kM, kDecBuf = kFrontWaves > 8 ? 1 : Cfg<DM>::kDecBuf;
+    constexpr int kM = Cfg<DM>::kM, kDecBuf = Cfg<DM>::kDecBuf;
     __shared__ __attribute__((aligned(16))) float2 Ms[kFrontWaves][kM];
     __shared__ __attribute__((aligned(16))) float2 decs[kFrontWaves][kDecBuf][kDec];
     __shared__ int mi_s[kGroups][2][QK_GROUP], rt_s[kGroups][2][QK_GROUP];
@@ -1623,7 +1622,7 @@ __global__ void __launch_bounds__((64 * kWavesOf<G, FP, MODE, DUAL, W, QUAD>),
         // fcnt[gi][p][b]: front waves done with block b of parity-p frames.
         constexpr int kBlkCh = W / kChainWaves;            // channels per block
         constexpr int kFrontChB = kBlkCh / kFrontPer;      // per front wave and block
-        static_assert(kBlkCh % kFrontPer == 0 || (kChainWaves == 1 && kGroups == 1), "block split");
+        static_assert(kBlkCh % kFrontPer == 0, "block split");
         if (wave < kBackWaves) {
             // ---------------------------------------------------- back of group
             // gi = (wave >> 1) / kChainWaves, block b, frames n = wave mod 2
@@ -1705,26 +1704,9 @@ __global__ void __launch_bounds__((64 * kWavesOf<G, FP, MODE, DUAL, W, QUAD>),
             // wave % 4) take s channels fewer, the others s more
             const int split = (kGroups == 1 && kChainWaves == 1) ? (a.roles >> 16) & 15 : 0;
             auto share = [&](int x) { return ((x + kBackWaves) & 3) < kBackWaves; };
-            int cbeg = 0, mych = 0;
-            if constexpr (kFrontPer != 8) {
-                // 1x10: the fronts on the two SIMDs without a back wave take
-                // `split` channels each (roles bits 16-19), the four beside a back
-                // wave share the rest
-                int nsh = 0;
-                for (int x = 0; x < kFrontPer; x++) nsh += share(x) ? 1 : 0;
-                const int rest = kBlkCh - (kFrontPer - nsh) * split;
-                auto cnt = [&](int x) {
-                    if (!share(x)) return split;
-                    int r = 0;
-                    for (int y = 0; y < x; y++) r += share(y) ? 1 : 0;
-                    return rest / nsh + (r < rest % nsh ? 1 : 0);
-                };
-                for (int x = 0; x < fl; x++) cbeg += cnt(x);
-                mych = cnt(fl);
-            } else {
-                for (int x = 0; x < fl; x++) cbeg += kFrontChB + (share(x) ? -split : split);
-                mych = kFrontChB + (share(fl) ? -split : split);
-            }
+            int cbeg = 0;
+            for (int x = 0; x < fl; x++) cbeg += kFrontChB + (share(x) ? -split : split);
+            const int mych = kFrontChB + (share(fl) ? -split : split);
             // this wave's channels of block bb: group index kBlkCh * bb + cbeg + c
             auto bch0 = [&](int bb) { return (grp0 + gi) * W + kBlkCh * bb + cbeg; };
             auto blive = [&](int bb) { return max(0, min(mych, a.nch - bch0(bb))); };
@@ -1916,7 +1898,7 @@ float bits2f(uint32_t u) {
 
 // rx_kernel instantiations (pick_shape below)
 struct Shape {
-    enum Kind { k4x2, k2x4d, k1x8d64, k1x8q16, k1x8q32, k1x10d64 };
+    enum Kind { k4x2, k2x4d, k1x8d64, k1x8q16, k1x8q32 };
     int kind;
     int roles;
 };
@@ -1965,7 +1947,6 @@ struct qpsk_ctx {
     // QPSK_DEBUG_STALL (tests)
     int roles = 3 | (1 << 4) | (kStagger << 8);
     int ncu = 256;              // compute units of the device
-    int split10 = 7;            // 1x10: channels per front on a SIMD without a back wave (QPSK_SPLIT10)
     int shape = -1;             // Shape::Kind forced by QPSK_SHAPE (A/B runs); -1: by batch size
     int width = 0;              // dual-chain group width forced by QPSK_WIDTH; 0: by batch size
     int prio = -1;              // issue priority forced by QPSK_PRIO (0 none, 1 front, 2 back)
@@ -2165,15 +2146,10 @@ extern "C" qpsk_ctx* qpsk_rx_create_mode(int device, int nch, int mode, int* err
     }
     if (const char* pv = getenv("QPSK_PRIO"))
         c->prio = !strcmp(pv, "none") ? 0 : !strcmp(pv, "front") ? 1 : !strcmp(pv, "back") ? 2 : -1;
-    if (const char* sv = getenv("QPSK_SPLIT10")) {
-        const int v = atoi(sv);
-        if (v >= 1 && v <= 10) c->split10 = v;
-    }
     if (const char* sh = getenv("QPSK_SHAPE")) {
         c->shape = !strcmp(sh, "4x2") ? Shape::k4x2
                  : !strcmp(sh, "2x4d") ? Shape::k2x4d
-                 : !strcmp(sh, "1x8") ? Shape::k1x8d64
-                 : !strcmp(sh, "1x10") ? Shape::k1x10d64 : -1;
+                 : !strcmp(sh, "1x8") ? Shape::k1x8d64 : -1;
     }
     int r = herr(hipSetDevice(device));
     if (r == QPSK_OK) {
@@ -2329,8 +2305,6 @@ static Shape pick_shape(const qpsk_ctx* c) {
         else if (W == 32) sh.kind = Shape::k1x8q32;
         else sh.roles = (sh.roles & ~((3 << 4) | (15 << 16))) | (2 << 4) | (2 << 16);
     }
-    if (sh.kind == Shape::k1x10d64)   // lane backs at back priority; 7 channels per back-free front
-        sh.roles = (sh.roles & ~((3 << 4) | (15 << 16))) | (2 << 4) | (c->split10 << 16);
     if (c->prio >= 0) sh.roles = (sh.roles & ~(3 << 4)) | (c->prio << 4);
     return sh;
 }
@@ -2390,7 +2364,7 @@ int qpsk_rx_launch(qpsk_ctx* c, const int16_t* d_in, int F, uint8_t* d_bits, uin
 #define QPSK_LAUNCH(GG, FF, MM, DD, WW, QQ, HH)                                                \
     hipLaunchKernelGGL((rx_kernel<GG, FF, MM, DD, WW, QQ, HH>),                                \
                        dim3((unsigned)((c->nch + (size_t)GG * WW - 1) / ((size_t)GG * WW))),   \
-                       dim3(64 * (kBackWavesOf<GG, FF, MM, DD, WW, QQ> + (GG) * (FF))), 0, s,  \
+                       dim3(64 * (kBackWavesOf<GG, FF, MM, DD, WW, QQ> + GG * FF)), 0, s,      \
                        d_in, c->d_hist, c->d_ptab,                                             \
                        c->d_ks, c->d_win[0], c->d_win[1], c->d_mi[0], c->d_mi[1], c->d_rt[0],  \
                        c->d_rt[1], d_bits, d_valid, d_trace, reinterpret_cast<float2*>(d_soft), \
@@ -2405,8 +2379,6 @@ int qpsk_rx_launch(qpsk_ctx* c, const int16_t* d_in, int F, uint8_t* d_bits, uin
             case Shape::k1x8d64: QPSK_LAUNCH(1, 8, MM, true, 64, false, HH); break;            \
             case Shape::k1x8q16: QPSK_LAUNCH(1, 8, MM, true, 16, true, HH); break;             \
             case Shape::k1x8q32: QPSK_LAUNCH(1, 8, MM, true, 32, true, HH); break;             \
-            /* 1x10: reference-size M only (dec752's M does not fit 10 fronts) */              \
-            case Shape::k1x10d64: QPSK_LAUNCH(1, (((MM) & 1) ? 8 : 10), MM, true, 64, false, HH); break; \
             default: QPSK_LAUNCH(4, 2, MM, false, 64, false, HH); break;                       \
         }                                                                                      \
     } while (0)

@@ -89,7 +89,7 @@ def test_fft_hunt_edge_inputs(mode):
     _vs_oracle(x, mode)
 
 
-@pytest.mark.parametrize("shape", ["4x2", "2x4d", "1x8", "1x10"])
+@pytest.mark.parametrize("shape", ["4x2", "2x4d", "1x8"])
 def test_fft_hunt_every_shape(shape, monkeypatch):
     monkeypatch.setenv("QPSK_SHAPE", shape)
     _vs_oracle(oracle.synth(66, 300, 10, 3.0), sc.MODE_FFT_HUNT)
