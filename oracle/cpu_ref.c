@@ -268,6 +268,7 @@ static int rx_frame(qc_chan_t *ch, const int16_t in[QC_FRAME], uint8_t bits[QC_B
                     qc_trace_t *tr, float (*dec_out)[2]);
 
 _Thread_local int qc_decision_step;
+int qc_poison_unobservable;
 
 int qc_rx_frame(qc_chan_t *ch, const int16_t in[QC_FRAME], uint8_t bits[QC_BITS],
                 qc_trace_t *tr) {
@@ -349,6 +350,11 @@ static int rx_frame(qc_chan_t *ch, const int16_t in[QC_FRAME], uint8_t bits[QC_B
     }
     }
 
+    if (qc_poison_unobservable) {   /* test switch, cpu_ref.h */
+        const float nan = bits2f(0x7fc00000u);
+        for (int j = 0; j < QC_DEC752; j++)
+            if (j < mi || j > mi + QC_PRE + QC_DSYM + 3) dec[j][0] = dec[j][1] = nan;
+    }
     /* equalize(), src/qpsk.c:111-123 */
     kal_t k;
     kal_reset(&k);

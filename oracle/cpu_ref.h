@@ -66,6 +66,12 @@ void qc_chan_init_mode(qc_chan_t *ch, int mode);
  * 30 misses); 128 if only the last step decided it.  Per thread (the batch
  * path runs qc_rx_frame on pthreads). */
 extern _Thread_local int qc_decision_step;
+/* Test switch (tests/test_oracle.py): when nonzero, every dec entry outside
+ * [mi, mi + 162] is set to NaN after the hunt, before the equalizer: the
+ * outputs must not change (the window's observable range, which the GPU's
+ * split FIR relies on: dec[255..289] only when mi >= 93).  Set it only while
+ * no call runs. */
+extern int qc_poison_unobservable;
 /* One qpsk_rx_frame() call.  bits[62] written (zero when invalid). */
 int qc_rx_frame(qc_chan_t *ch, const int16_t in[QC_FRAME], uint8_t bits[QC_BITS],
                 qc_trace_t *tr);

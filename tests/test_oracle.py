@@ -42,6 +42,34 @@ def test_sample_file_md5(golden_dir):
     np.testing.assert_array_equal(tr[0]["soft"][vm], st["soft"][vm])
 
 
+@pytest.mark.parametrize("ebn0", [1000.0, 8.0, 3.0, 0.0])
+def test_window_observable_range(ebn0):
+    """The equalizer and the data symbols read only dec[mi .. mi + 162]
+    (src/qpsk.c:188, 204-215: 128 training steps and 31 data steps, 5 taps):
+    with every other entry of the frame's dec set to NaN after the hunt
+    (qc_poison_unobservable) the restatement's outputs, soft symbols included,
+    do not change.  This is what lets the GPU's split FIR compute dec[255..289]
+    only when mi >= 93 ("the split FIR")."""
+    import ctypes
+    flag = ctypes.c_int.in_dll(oracle.cpu_lib(), "qc_poison_unobservable")
+    rng = np.random.default_rng(9)
+    x = oracle.synth(91, 96, 10, ebn0)
+    x[0] = 0                                          # silence
+    x[1, 3:5] = 32767                                 # saturated frames
+    x[2] = rng.integers(-32768, 32768, x[2].shape)    # full-scale noise
+    b1, v1, t1 = oracle.cpu_rx(x, trace=True)
+    flag.value = 1
+    try:
+        b2, v2, t2 = oracle.cpu_rx(x, trace=True)
+    finally:
+        flag.value = 0
+    np.testing.assert_array_equal(v1, v2)
+    np.testing.assert_array_equal(b1, b2)
+    np.testing.assert_array_equal(t1.view(np.uint8), t2.view(np.uint8))   # incl. soft, bitwise
+    mi = t1["max_index"][v1.astype(bool)]
+    assert v1.sum() > 0 and (ebn0 < 5 or (mi >= 93).any())
+
+
 def test_mixer_table_kat(golden_dir):
     """P[t] = R^(t+1) (src/qpsk.c:139) and the (-1)^n frame alternation."""
     kat = np.load(os.path.join(golden_dir, "kat.npz"))
