@@ -28,6 +28,7 @@
 
 #include <algorithm>
 #include <utility>
+#include <vector>
 
 #include "qpsk_batch.h"
 #include "qpsk_fft.h"
@@ -529,10 +530,62 @@ __device__ __forceinline__ f2 fir_one(const float2* b) {
 // 392 packed operations before the hunt (294 + 98) instead of 490, and 98 more
 // for the ~27% of channels whose window reaches past dec[254].
 constexpr int kSplitMi = 255 - (QK_NPRE + QK_NDSYM + 3);   // 93: mi + 162 >= 255
-__device__ __forceinline__ void fir_split(int lane, int rt, const float2* M, float2* dec) {
+// LDS banks (ds_read_b64: lanes 0-31 and 32-63 are serviced apart, float2 f in
+// bank pair f mod 32; MI355X_MICROARCH.md "LDS").  Pass 1's lanes 32..62 read
+// M[15l + rt + s]: 31 distinct pairs, so lane 63's base must be the 32nd,
+// (15*63 + rt) mod 32; its outputs F[j1], F[j1+5], F[j1+10] follow from that
+// residue r: j1 = r + 32 (r <= 24) or r (both <= 56).  Pass 2 reads M[kM1 + j
+// + s] for the 64 other j of [0, 66]: lanes 32..63 take j = 35..66 with each of
+// pass 1's j in that range replaced by j - 32 (one j per bank pair), lanes 0..31
+// the rest.  [0, 66] holds the pairs of j = 0, 1, 2 three times and pass 1's
+// triple is 5 apart, so one lane group always keeps a 2-way conflict: 49 extra
+// LDS cycles per channel in pass 2, none in pass 1 (before this mapping: pass 1
+// lane 63 at F[56] collided for 31 of 32 rt mod 32, and pass 2's j = 64, 65
+// with j = 32, 33 -- profiles/probe/fir_split_banks.py).
+// QPSK_SPLIT_BANKS 0: the round-5 mapping (A/B knob).
+#ifndef QPSK_SPLIT_BANKS
+#define QPSK_SPLIT_BANKS 1
+#endif
+__host__ __device__ constexpr int split_r(int rt) { return (15 * 63 + rt - kM1) & 31; }
+__host__ __device__ constexpr int split_j1(int r) { return r <= 24 ? r + 32 : r; }
+struct SplitTab {
+    uint8_t j[32][64];   // [r][lane]: pass 2's output F[j]
+};
+constexpr SplitTab make_split_tab() {
+    SplitTab t{};
+    for (int r = 0; r < 32; r++) {
+        const int j1 = split_j1(r);
+        bool used[67] = {};
+        used[j1] = used[j1 + 5] = used[j1 + 10] = true;
+        for (int i = 0; i < 32; i++) {
+            const int v = 35 + i;
+            const int j = (v == j1 || v == j1 + 5 || v == j1 + 10) ? v - 32 : v;
+            t.j[r][32 + i] = (uint8_t)j;
+            used[j] = true;
+        }
+        int l = 0;
+        for (int v = 0; v < 67; v++)
+            if (!used[v]) t.j[r][l++] = (uint8_t)v;
+    }
+    return t;
+}
+__constant__ SplitTab kSplitTab = make_split_tab();
+constexpr int kSplitTabWords = QPSK_SPLIT_BANKS ? (int)sizeof(SplitTab) / 4 : 1;
+
+__device__ __forceinline__ void fir_split(int lane, int rt, const float2* M, float2* dec,
+                                          const uint8_t* p2tab) {
     lane = fresh_lane(lane);   // the per-lane bases below are recomputed, not kept live across the loop
+#if QPSK_SPLIT_BANKS
+    const int r = split_r(__builtin_amdgcn_readfirstlane(rt));
+    const int j1 = split_j1(r);
+    const int j2 = p2tab[r * 64 + lane];
+#else
+    (void)p2tab;
+    constexpr int j1 = 56;
+    const int j2 = lane + (lane >= 56 ? 1 : 0) + (lane >= 60 ? 1 : 0);
+#endif
     {   // pass 1
-        const float2* b = lane < 63 ? M + 15 * lane + rt : M + kM1 + 56;
+        const float2* b = lane < 63 ? M + 15 * lane + rt : M + kM1 + j1;
         f2 y[3] = {{0.0f, 0.0f}, {0.0f, 0.0f}, {0.0f, 0.0f}};
 #pragma unroll
         for (int s0 = 0; s0 < 59; s0 += QPSK_FB) {
@@ -558,14 +611,13 @@ __device__ __forceinline__ void fir_split(int lane, int rt, const float2* M, flo
 #pragma unroll
         for (int m = 0; m < 3; m++) {
             const f2 o = y[m] * QK_GAIN;
-            const int d = lane < 63 ? 3 * lane + m : QK_NDEC + 56 + 5 * m;
+            const int d = lane < 63 ? 3 * lane + m : QK_NDEC + j1 + 5 * m;
             if (d < QK_NDEC || lane == 63) dec[d] = make_float2(o.x, o.y);
         }
     }
     {   // pass 2
-        const int j = lane + (lane >= 56 ? 1 : 0) + (lane >= 60 ? 1 : 0);
-        const f2 o = fir_one(M + kM1 + j);
-        dec[QK_NDEC + j] = make_float2(o.x, o.y);
+        const f2 o = fir_one(M + kM1 + j2);
+        dec[QK_NDEC + j2] = make_float2(o.x, o.y);
     }
 }
 
@@ -703,7 +755,8 @@ __device__ __forceinline__ int hunt(int lane, float2* M, const float2* dec, cons
 // `head` (global, 51 x 16 B), instead of the head FIR.
 template <int MODE, bool HP = false, bool SPLIT = false>
 __device__ __forceinline__ int front_channel(int lane, int rt, float2* M, float2* dec,
-                                             const float* BT, const float2* head FACC_PARAM) {
+                                             const float* BT, const uint8_t* p2tab,
+                                             const float2* head FACC_PARAM) {
 #ifdef QPSK_STAMPS
     unsigned long long ft0 = stamp_now();
 #endif
@@ -717,7 +770,7 @@ __device__ __forceinline__ int front_channel(int lane, int rt, float2* M, float2
         FSTAMP(0);
         if (lane < kHeadOut / 2) *reinterpret_cast<float4*>(dec + QK_NDEC + 2 * lane) = h;
     } else if constexpr (MODE == 0 && SPLIT) {
-        fir_split(lane, rt, M, dec);   // dec[0..254]
+        fir_split(lane, rt, M, dec, p2tab);   // dec[0..254]
         FSTAMP(0);
         wave_lds_sync();
         FSTAMP(1);
@@ -1577,6 +1630,10 @@ __global__ void __launch_bounds__((64 * kWavesOf<G, FP, MODE, DUAL, W, QUAD>),
     __shared__ int mi_s[kGroups][2][QK_GROUP], rt_s[kGroups][2][QK_GROUP];
     // hunt tables: the MFMA correlator's B, or the FFT hunt's twiddles / Q / permutation
     __shared__ __attribute__((aligned(16))) float BT[(MODE & 2) ? kFftHT : kHuntTab];
+    // the split FIR's pass-2 lane map (kSplitTab; 2 KB, reference mode only)
+    constexpr bool kSplitK = MODE == 0 && !HP && QPSK_FIR_SPLIT && (!DUAL || QPSK_FIR_SPLIT == 2);
+    __shared__ uint32_t p2w[kSplitK ? kSplitTabWords : 1];
+    const uint8_t* p2tab = reinterpret_cast<const uint8_t*>(p2w);
     // DUAL progress counters, per group, frame parity and channel block (one
     // block per back wave of a chain)
     __shared__ int bseq[kGroups][2][kChainWaves], fcnt[kGroups][2][kChainWaves];
@@ -1589,6 +1646,9 @@ __global__ void __launch_bounds__((64 * kWavesOf<G, FP, MODE, DUAL, W, QUAD>),
     const int grp0 = blockIdx.x * kGroups;
     for (int i = threadIdx.x; i < QK_FRAME / 2; i += kBlock)
         reinterpret_cast<float4*>(P)[i] = reinterpret_cast<const float4*>(a.ptab)[i];
+    if constexpr (kSplitK && QPSK_SPLIT_BANKS)
+        for (int i = threadIdx.x; i < kSplitTabWords; i += kBlock)
+            p2w[i] = reinterpret_cast<const uint32_t*>(&kSplitTab)[i];
     if constexpr ((MODE & 2) != 0) {
         for (int i = threadIdx.x; i < kFftHT; i += kBlock) BT[i] = fft_tab[i];
     } else {
@@ -1760,7 +1820,7 @@ __global__ void __launch_bounds__((64 * kWavesOf<G, FP, MODE, DUAL, W, QUAD>),
                 }                                                                                              \
                 wave_lds_sync();                                                                               \
                 STAMP(1);                                                                                      \
-                pmi = front_channel<MODE, HP, kSplitD>(lane, rt_s[gi][p][i0 + c], M, dcur, BT,                 \
+                pmi = front_channel<MODE, HP, kSplitD>(lane, rt_s[gi][p][i0 + c], M, dcur, BT, p2tab,         \
                                               a.heads + ((size_t)ch * a.F + n) * kHeadOut FACC_ARG);           \
                 if (lane == 0) mi_s[gi][p ^ 1][i0 + c] = pmi;                                                  \
                 if (c + 1 == nl) store_window(lane, pmi, dcur, wout + (size_t)ch * kWinStride);                \
@@ -1871,7 +1931,7 @@ __global__ void __launch_bounds__((64 * kWavesOf<G, FP, MODE, DUAL, W, QUAD>),
                 }
                 wave_lds_sync();
                 STAMP(1);
-                pmi = front_channel<MODE, HP, kSplit>(lane, rt_s[gi][p][cbeg + c], M, dcur, BT,
+                pmi = front_channel<MODE, HP, kSplit>(lane, rt_s[gi][p][cbeg + c], M, dcur, BT, p2tab,
                                               a.heads + ((size_t)ch * a.F + n) * kHeadOut FACC_ARG);
                 if (lane == 0) mi_s[gi][p ^ 1][cbeg + c] = pmi;
                 if (c + 1 == nlive) store_window(lane, pmi, dcur, wout + (size_t)ch * kWinStride);
@@ -1970,19 +2030,28 @@ extern "C" int qpsk_rx_timing_split(qpsk_ctx* c, float* ms_rx, float* ms_data, i
 static int herr(hipError_t e) { return e == hipSuccess ? QPSK_OK : QPSK_EHIP - (int)e; }
 #define HCHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) return herr(e_); } while (0)
 
-static void build_tables(float2* ptab, unsigned long long* ksf) {
+// The receiver's constant tables, built once per process on first use (a C++11
+// function-local static: its initialisation is thread-safe, and contexts
+// created from several host threads at once share the one read-only copy).
+struct RxTables {
+    float2 ptab[QK_FRAME];                 // P[t] * 2^-14
+    unsigned long long ksf[QK_KS_FRAMES];  // keystream bits of frame f, 62 per word
+};
+
+static RxTables* make_rx_tables() {
+    RxTables* t = new RxTables();
     // P[t] = R^(t+1): fbb_rx_phase *= fbb_rx_rect (src/qpsk.c:139), fp32, host
     const float rr = bits2f(QK_RX_RECT_RE_BITS), ri = bits2f(QK_RX_RECT_IM_BITS);
     volatile float pr = 1.0f, pi = 0.0f;  // volatile: keep every op a rounded fp32 op
-    for (int t = 0; t < QK_FRAME; t++) {
+    for (int k = 0; k < QK_FRAME; k++) {
         const float a = pr * rr - pi * ri;
         const float b = pr * ri + pi * rr;
         pr = a;
         pi = b;
-        ptab[t] = make_float2(a * 0x1p-14f, b * 0x1p-14f);  // exact power-of-two scale
+        t->ptab[k] = make_float2(a * 0x1p-14f, b * 0x1p-14f);  // exact power-of-two scale
     }
     // keystream of the RX descrambler (src/scramble.c:57-69), 62 bits per frame
-    static uint8_t ks[QK_KS_PERIOD];
+    std::vector<uint8_t> ks(QK_KS_PERIOD);
     uint16_t m = QK_SEED;
     for (int k = 0; k < QK_KS_PERIOD; k++) {
         const uint16_t o = (uint16_t)(((m & 2) >> 1) ^ (m & 1));
@@ -1993,8 +2062,14 @@ static void build_tables(float2* ptab, unsigned long long* ksf) {
         unsigned long long w = 0;
         for (int b = 0; b < QK_NBITS; b++)
             w |= (unsigned long long)ks[(62 * f + b) % QK_KS_PERIOD] << b;
-        ksf[f] = w;
+        t->ksf[f] = w;
     }
+    return t;
+}
+
+static const RxTables& rx_tables() {
+    static const RxTables* const t = make_rx_tables();   // never freed: process lifetime
+    return *t;
 }
 
 // state arrays cover whole workgroups of the largest shape (kMaxGroups groups)
@@ -2161,11 +2236,9 @@ extern "C" qpsk_ctx* qpsk_rx_create_mode(int device, int nch, int mode, int* err
     if (r == QPSK_OK) r = herr(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     if (r == QPSK_OK) r = ctx_alloc(c);
     if (r == QPSK_OK) {
-        static float2 ptab[QK_FRAME];
-        static unsigned long long ksf[QK_KS_FRAMES];
-        build_tables(ptab, ksf);
-        r = herr(hipMemcpy(c->d_ptab, ptab, sizeof ptab, hipMemcpyHostToDevice));
-        if (r == QPSK_OK) r = herr(hipMemcpy(c->d_ks, ksf, sizeof ksf, hipMemcpyHostToDevice));
+        const RxTables& t = rx_tables();
+        r = herr(hipMemcpy(c->d_ptab, t.ptab, sizeof t.ptab, hipMemcpyHostToDevice));
+        if (r == QPSK_OK) r = herr(hipMemcpy(c->d_ks, t.ksf, sizeof t.ksf, hipMemcpyHostToDevice));
     }
     if (r == QPSK_OK && (mode & QPSK_MODE_FFT_HUNT)) r = fft_hunt_tables(c);
     if (r == QPSK_OK) r = qpsk_rx_reset(c);

@@ -259,6 +259,10 @@ def test_split_fir_window_boundary(monkeypatch):
     out = _vs_oracle(x)
     mi = out["trace"][..., 0][out["valid"].astype(bool)]
     assert (mi >= 93).sum() > 20 and ((mi < 93) & (mi >= 80)).sum() > 5, np.bincount(mi)
+    # pass 1's lane 63 and pass 2's lane map follow rx_timing mod 32 (the LDS
+    # bank pair lanes 32..62 leave free, qpsk_rx.hip split_r): every residue ran
+    rt_in = np.concatenate([np.full((x.shape[0], 1), 3), out["trace"][:, :-1, 3]], axis=1)
+    assert len(np.unique((rt_in - 295) & 31)) == 32
 
 
 @pytest.mark.parametrize("width", ["16", "32", "64"])
