@@ -103,6 +103,7 @@ def ref_lib(mode: int = MODE_REF):
         lib.ref_rx_batch.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
         lib.ref_layout_gap.restype = C.c_long
         lib.ref_log_set.argtypes = [C.c_void_p, C.c_size_t]
+        lib.ref_poison_set.argtypes = [C.c_int, C.c_int, C.c_int]
         _ref[mode] = lib
     return _ref[mode]
 
@@ -147,6 +148,18 @@ def ref_rx(x, trace: bool = False, log: bool = False, mode: int = MODE_REF):
     if log:
         lib.ref_log_set(None, 0)
     return (bits, valid, tr, buf.value.decode()) if log else (bits, valid, tr)
+
+
+def ref_rx_poisoned(x, lo: int, hi: int, mode: int = MODE_REF):
+    """ref_rx with the observability probe on: before each frame's equalizer
+    the reference's decimated_frame[0..289] outside [mi + lo, mi + hi] is NaN
+    (oracle/ref/ref_trace.c ref_poison_set)."""
+    lib = ref_lib(mode)
+    lib.ref_poison_set(1, lo, hi)
+    try:
+        return ref_rx(x, trace=True, mode=mode)
+    finally:
+        lib.ref_poison_set(0, 0, 0)
 
 
 def ref_stages(x, mode: int = MODE_REF):

@@ -51,6 +51,10 @@ int ref_tx_frame(int16_t *out, const float *sym, int len, int preamble);
 /* Byte distance between decimated_frame and input_frame in this build. */
 long ref_layout_gap(void);
 
+/* Observability probe: NaN decimated_frame[0..289] outside [mi + lo, mi + hi]
+ * before each frame's equalizer (on != 0), see ref_trace.c. */
+void ref_poison_set(int on, int lo, int hi);
+
 void ref_trace_begin(ref_trace_t *tr);
 void ref_trace_end(void);
 void ref_log_set(char *buf, size_t cap);

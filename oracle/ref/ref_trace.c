@@ -61,7 +61,27 @@ int ref_debug_printf(const char *fmt, ...) {
     return n;
 }
 
+/* Observability probe (tests/test_oracle.py::test_window_observable_range_
+ * in_the_reference): when set, before a frame's first train_eq -- after the
+ * hunt, src/qpsk.c:172-188 -- every entry of decimated_frame[0..289] (the
+ * frame's own dec: the next call rewrites [0, 376) from [376, 752)) outside
+ * [index + lo, index + hi] is set to NaN.  index is max_index.  This changes
+ * the reference's data, never its code: a probe of which entries reach an
+ * output, not a trace. */
+static int g_poison, g_plo, g_phi;
+
+void ref_poison_set(int on, int lo, int hi) {
+    g_poison = on;
+    g_plo = lo;
+    g_phi = hi;
+}
+
 float __wrap_train_eq(complex float in[], int index, float ref) {
+    if (g_poison && g_train_calls == 0) {
+        const float nan = __builtin_nanf("");
+        for (int k = 0; k < 290; k++)
+            if (k < index + g_plo || k > index + g_phi) in[k] = CMPLXF(nan, nan);
+    }
     float r = __real_train_eq(in, index, ref);
     if (g_tr) {
         if (g_train_calls == 0) g_tr->max_index = index;

@@ -70,6 +70,48 @@ def test_window_observable_range(ebn0):
     assert v1.sum() > 0 and (ebn0 < 5 or (mi >= 93).any())
 
 
+@pytest.mark.skipif(not oracle.ref_available(), reason="reference build not present")
+def test_window_observable_range_in_the_reference(golden_dir):
+    """The split FIR's premise, pinned on the unmodified reference itself
+    (oracle/_ref, the -Wl,--wrap=train_eq tap): with decimated_frame[0..289]
+    set to NaN outside [mi, mi + 162] before each frame's equalizer
+    (/root/reference/src/qpsk.c:186-215, after the hunt), the reference's
+    outputs -- valid flags, bits, max_index, matches, rx_timing, and the soft
+    symbols of valid frames, bitwise -- do not change on the sample file and
+    seeded noiseless / AWGN sets; with one entry fewer at either end
+    ([mi + 1, mi + 162] or [mi, mi + 161]) they do.  (Invalid frames' data_eq
+    runs at rx_timing, src/qpsk.c:225-229, and its soft symbols are no output:
+    they are compared on valid frames only.)"""
+    rng = np.random.default_rng(19)
+    sets = [_sample(golden_dir)]
+    for seed, eb in ((92, 1000.0), (93, 8.0), (94, 3.0), (95, 0.0)):
+        sets.append(oracle.synth(seed, 24, 10, eb))
+    sets[-1][0] = 0                                          # silence
+    sets[-1][1, 3:5] = 32767                                 # saturated frames
+    sets[-1][2] = rng.integers(-32768, 32768, sets[-1][2].shape)   # full-scale noise
+
+    def outputs(r):
+        bits, valid, tr = r
+        vm = valid.astype(bool)
+        return (valid, bits, tr["max_index"], tr["matches"], tr["rx_timing"],
+                tr["soft"][vm].view(np.uint32))
+
+    nvalid = nhigh = 0
+    narrower = {(1, 162): 0, (0, 161): 0}
+    for x in sets:
+        base = outputs(oracle.ref_rx(x, trace=True))
+        for a, b in zip(base, outputs(oracle.ref_rx_poisoned(x, 0, 162))):
+            np.testing.assert_array_equal(a, b)
+        for lohi in narrower:
+            got = outputs(oracle.ref_rx_poisoned(x, *lohi))
+            narrower[lohi] += sum(not np.array_equal(a, b) for a, b in zip(base, got))
+        vm = base[0].astype(bool)
+        nvalid += int(vm.sum())
+        nhigh += int((base[2][vm] >= 93).sum())
+    assert nvalid > 50 and nhigh > 5           # windows reaching past dec[254] ran
+    assert all(v > 0 for v in narrower.values()), narrower
+
+
 def test_mixer_table_kat(golden_dir):
     """P[t] = R^(t+1) (src/qpsk.c:139) and the (-1)^n frame alternation."""
     kat = np.load(os.path.join(golden_dir, "kat.npz"))
