@@ -113,10 +113,20 @@ uint64_t qpsk_rx_frames(const qpsk_ctx *ctx);
  * one 16-frame call.  The frame index is shared by all channels of a
  * context: a context takes the snapshot's index when it has received no
  * frame since create/reset (qpsk_rx_frames() == 0); otherwise the indices
- * must be equal (QPSK_EINVAL).  Both calls wait for the context's calls in
+ * must be equal (QPSK_EINVAL).  Loading fewer than all channels into such a
+ * fresh context from a snapshot at frame G != 0 moves every channel to frame
+ * G, so the context then receives nothing (qpsk_rx_batch*, streams, state
+ * saves: QPSK_EINVAL) until each of its channels has been loaded from
+ * snapshots at G (any number of ranges, in any order); qpsk_rx_reset()
+ * abandons such an assembly.  Both calls wait for the context's calls in
  * flight; on a stream's context they return QPSK_EBUSY while chunks are
  * pending.  n snapshots' channel ranges may differ from the ones loaded into
- * (channel c0 + i of the snapshot goes to channel c0' + i). */
+ * (channel c0 + i of the snapshot goes to channel c0' + i).
+ * qpsk_rx_state_save returns QPSK_ESTALL once any call of the context has
+ * stalled since create/reset (reported, or still in the device error word,
+ * which it reads without taking): that state is undefined.  A snapshot is a
+ * function of the channels' state alone (window slots past the last one the
+ * equalizer reads are zero). */
 size_t qpsk_rx_state_size(int n);
 int qpsk_rx_state_save(qpsk_ctx *ctx, int c0, int n, void *buf, size_t size);
 int qpsk_rx_state_load(qpsk_ctx *ctx, int c0, int n, const void *buf, size_t size);

@@ -51,4 +51,14 @@ bw = nch // 64   # back waves
 btot = int(st[13]) + int(st[14])
 out["back_cycles_per_frame"] = {bnames[i]: round(int(st[i]) / (bw * nf), 1) for i in (13, 14)}
 out["back_share"] = {bnames[i]: round(int(st[i]) / max(btot, 1), 3) for i in (13, 14)}
+# round 6 (4x2 only): the back wave's arrival at the frame barrier minus the
+# last arrival of the fronts on its SIMD (stamp 15), over the frames where the
+# back arrived last (stamp 5): the cycles it trains alone at each frame's end
+fr = bw * nf
+out["back_alone_tail"] = {
+    "frames_back_last_share": round(int(st[5]) / fr, 3),
+    "tail_cycles_per_frame_all": round(int(st[15]) / fr, 1),
+    "tail_cycles_per_frame_when_last": round(int(st[15]) / max(int(st[5]), 1), 1),
+    "frame_cycles": round(btot / fr, 1),
+    "tail_share_of_frame": round(int(st[15]) / max(btot, 1), 3)}
 print(json.dumps(out, indent=1))

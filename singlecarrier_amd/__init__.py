@@ -231,6 +231,8 @@ class Receiver:
         """Load a snapshot of n channels into channels [c0, c0 + n)
         (qpsk_rx_state_load)."""
         buf = np.frombuffer(snap, np.uint8)
+        if len(snap) < 64 or bytes(snap[:8]) != b"QPSKSTA1":   # StateHdr: 64 bytes, magic first
+            _check(QPSK_EINVAL)
         if n is None:
             n = int(np.frombuffer(snap[20:24], np.int32)[0])   # StateHdr.n
         _check(lib().qpsk_rx_state_load(self._h, c0, n, _ptr(buf), buf.size))

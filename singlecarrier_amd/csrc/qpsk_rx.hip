@@ -1639,11 +1639,33 @@ __global__ void __launch_bounds__((64 * kWavesOf<G, FP, MODE, DUAL, W, QUAD>),
     __shared__ int bseq[kGroups][2][kChainWaves], fcnt[kGroups][2][kChainWaves];
     __shared__ int dead_s;                               // DUAL: a wait of this workgroup timed out
     __shared__ int nwait_s;                              // kDyn: back waves waiting for their fronts
+#ifdef QPSK_STAMPS
+    // diagnostic (4x2): each wave's arrival at the frame barrier and its SIMD;
+    // a back wave sums the cycles it trains after the last front of its SIMD
+    // arrived (stamp 15) and counts the frames it arrived last (stamp 5)
+    __shared__ unsigned long long tarr_s[16];
+    __shared__ int tsimd_s[16];
+#define TAIL_INIT() do { if (lane == 0 && wave < 16) tsimd_s[wave] = (int)((__builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4) >> 4) & 3); } while (0)
+#define TAIL_ARRIVE() do { if (lane == 0 && wave < 16) tarr_s[wave] = stamp_now(); } while (0)
+#define TAIL_BACK()                                                                           \
+    do {                                                                                      \
+        unsigned long long tf = 0;                                                            \
+        for (int w2 = kBackWaves; w2 < kBackWaves + kFrontWaves && w2 < 16; w2++)             \
+            if (tsimd_s[w2] == tsimd_s[wave] && tarr_s[w2] > tf) tf = tarr_s[w2];            \
+        if (tf > 0 && tarr_s[wave] > tf) { st_acc[15] += tarr_s[wave] - tf; st_acc[5] += 1; } \
+        st_t0 = stamp_now();                                                                  \
+    } while (0)
+#else
+#define TAIL_INIT() do { } while (0)
+#define TAIL_ARRIVE() do { } while (0)
+#define TAIL_BACK() do { } while (0)
+#endif
     const int lane = threadIdx.x & 63;
     // wave-uniform by construction; readfirstlane tells the compiler, so every
     // per-wave index and pointer below lives in SGPRs
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int grp0 = blockIdx.x * kGroups;
+    TAIL_INIT();
     for (int i = threadIdx.x; i < QK_FRAME / 2; i += kBlock)
         reinterpret_cast<float4*>(P)[i] = reinterpret_cast<const float4*>(a.ptab)[i];
     if constexpr (kSplitK && QPSK_SPLIT_BANKS)
@@ -1879,8 +1901,10 @@ __global__ void __launch_bounds__((64 * kWavesOf<G, FP, MODE, DUAL, W, QUAD>),
             else
                 rt_s[gi][p ^ 1][lane] = rt_s[gi][p][lane];
             STAMP(13);
+            TAIL_ARRIVE();
             __syncthreads();
             STAMP(14);
+            TAIL_BACK();
         }
         STAMP_FLUSH();
         if (live) {   // per-channel state after the call's last frame
@@ -1938,6 +1962,7 @@ __global__ void __launch_bounds__((64 * kWavesOf<G, FP, MODE, DUAL, W, QUAD>),
                 wave_lds_sync();
                 STAMP(6);
             }
+            TAIL_ARRIVE();
             __syncthreads();
             STAMP(7);
         }
@@ -2023,6 +2048,15 @@ struct qpsk_ctx {
     int stall_calls = -1;       // QPSK_DEBUG_STALL=first: the stall only in the first launch; -1: every call
     uint64_t launches = 0;      // calls launched over the context's life (qpsk_rx_reset keeps it)
     const qpsk_stream* owner = nullptr;   // the stream this context belongs to, if any
+    // a call reported QPSK_ESTALL since the last reset: the per-channel state
+    // is undefined, and qpsk_rx_state_save refuses to export it
+    bool stalled = false;
+    // qpsk_rx_state_load of a channel range into a fresh context (frame 0) from
+    // a snapshot at frame G != 0: the context takes frame index G, so every
+    // channel must be loaded before it may receive (asm_left channels to go;
+    // asm_cover marks the loaded ones)
+    std::vector<uint8_t> asm_cover;
+    int asm_left = 0;
 };
 
 extern "C" int qpsk_rx_timing_split(qpsk_ctx* c, float* ms_rx, float* ms_data, int* frames);
@@ -2119,12 +2153,18 @@ extern "C" int qpsk_rx_reset(qpsk_ctx* c) {
     c->frames = 0;
     c->calls = 0;
     c->epoch++;
+    c->stalled = false;
+    c->asm_cover.clear();
+    c->asm_left = 0;
     return QPSK_OK;
 }
 
 int* qpsk_rx_err_word(qpsk_ctx* c) { return c ? c->d_err : nullptr; }
 void qpsk_rx_set_owner(qpsk_ctx* c, const qpsk_stream* s) { if (c) c->owner = s; }
 uint64_t qpsk_rx_epoch(const qpsk_ctx* c) { return c ? c->epoch : 0; }
+void qpsk_rx_mark_stalled(qpsk_ctx* c, uint64_t epoch) {
+    if (c && epoch == c->epoch) c->stalled = true;
+}
 
 static void ctx_free(qpsk_ctx* c) {
     for (int i = 0; i < qpsk_ctx::kEv; i++)
@@ -2273,6 +2313,8 @@ struct StateHdr {
 static_assert(sizeof(StateHdr) == 64, "state header");
 constexpr size_t kHistB = sizeof(int16_t) * 2 * QK_FRAME, kWinB = sizeof(float2) * kWinStride;
 constexpr size_t kChanB = kHistB + kWinB + 2 * sizeof(int);
+constexpr int kWinObs = QK_NPRE + QK_NDSYM + 5;   // slots 0..163 = dec[mi-1 .. mi+162]
+static_assert(kWinObs == 164 && kWinObs <= kWinStride, "window slots");
 }  // namespace
 
 extern "C" size_t qpsk_rx_state_size(int n) { return n < 1 ? 0 : sizeof(StateHdr) + (size_t)n * kChanB; }
@@ -2289,6 +2331,17 @@ static int state_begin(qpsk_ctx* c, int c0, int n, const void* buf, size_t size)
 extern "C" int qpsk_rx_state_save(qpsk_ctx* c, int c0, int n, void* buf, size_t size) {
     int r = state_begin(c, c0, n, buf, size);
     if (r != QPSK_OK) return r;
+    // channels still to be loaded (qpsk_rx_state_load) hold no state of frame G
+    if (c->asm_left > 0) return QPSK_EINVAL;
+    // a stall (reported, or still in the error word: peeked, not taken, so
+    // qpsk_rx_sync still reports it) leaves the state undefined
+    if (!c->stalled) {
+        int e = 0;
+        HCHECK(hipMemcpyAsync(&e, c->d_err, sizeof e, hipMemcpyDeviceToHost, c->stream));
+        HCHECK(hipStreamSynchronize(c->stream));
+        if (e != 0) return QPSK_ESTALL;
+    }
+    if (c->stalled) return QPSK_ESTALL;
     StateHdr h{};
     memcpy(h.magic, kStateMagic, sizeof h.magic);
     h.version = 1;
@@ -2305,12 +2358,19 @@ extern "C" int qpsk_rx_state_save(qpsk_ctx* c, int c0, int n, void* buf, size_t 
     const size_t nn = (size_t)n;
     HCHECK(hipMemcpyAsync(o, c->d_hist + (size_t)c0 * 2 * QK_FRAME, nn * kHistB, hipMemcpyDeviceToHost, c->stream));
     o += nn * kHistB;
+    char* w = o;
     HCHECK(hipMemcpyAsync(o, c->d_win[p] + (size_t)c0 * kWinStride, nn * kWinB, hipMemcpyDeviceToHost, c->stream));
     o += nn * kWinB;
     HCHECK(hipMemcpyAsync(o, c->d_mi[p] + c0, nn * sizeof(int), hipMemcpyDeviceToHost, c->stream));
     o += nn * sizeof(int);
     HCHECK(hipMemcpyAsync(o, c->d_rt[p] + c0, nn * sizeof(int), hipMemcpyDeviceToHost, c->stream));
     HCHECK(hipStreamSynchronize(c->stream));
+    // window slots past dec[mi+162] (the last data symbol's taps, SURVEY.md
+    // A.6) are never read; the fronts leave whatever their dec buffer held
+    // there (the split FIR skips dec[255..289] when mi < 93).  Zeroed, so a
+    // snapshot is a function of the channel's state alone.
+    for (size_t i = 0; i < nn; i++)
+        memset(w + i * kWinB + kWinObs * sizeof(float2), 0, (kWinStride - kWinObs) * sizeof(float2));
     return QPSK_OK;
 }
 
@@ -2323,6 +2383,10 @@ extern "C" int qpsk_rx_state_load(qpsk_ctx* c, int c0, int n, const void* buf, s
         h.n != n || h.mode != c->mode || h.hist_bytes != kHistB || h.win_bytes != kWinB)
         return QPSK_EINVAL;
     if (c->frames != h.frame && c->frames != 0) return QPSK_EINVAL;   // one frame index per context
+    // a channel range at frame G != 0 into a fresh context moves the context's
+    // frame index to G for every channel: the others must be loaded too
+    // (from this or other snapshots at G) before the context may receive
+    const bool assemble = c->asm_left > 0 || (c->frames == 0 && h.frame != 0 && n < c->nch);
     const char* o = static_cast<const char*>(buf) + sizeof h;
     const int p = (int)(h.frame & 1u);
     const size_t nn = (size_t)n;
@@ -2334,6 +2398,18 @@ extern "C" int qpsk_rx_state_load(qpsk_ctx* c, int c0, int n, const void* buf, s
     o += nn * sizeof(int);
     HCHECK(hipMemcpyAsync(c->d_rt[p] + c0, o, nn * sizeof(int), hipMemcpyHostToDevice, c->stream));
     HCHECK(hipStreamSynchronize(c->stream));
+    if (assemble) {
+        if (c->asm_cover.empty()) {
+            c->asm_cover.assign((size_t)c->nch, 0);
+            c->asm_left = c->nch;
+        }
+        for (int i = c0; i < c0 + n; i++)
+            if (!c->asm_cover[(size_t)i]) {
+                c->asm_cover[(size_t)i] = 1;
+                c->asm_left--;
+            }
+        if (c->asm_left == 0) c->asm_cover.clear();
+    }
     c->frames = h.frame;
     return QPSK_OK;
 }
@@ -2389,6 +2465,7 @@ static Shape pick_shape(const qpsk_ctx* c) {
 int qpsk_rx_launch(qpsk_ctx* c, const int16_t* d_in, int F, uint8_t* d_bits, uint8_t* d_valid,
                    int32_t* d_trace, float* d_soft, hipStream_t s, int* d_err, int* err_to) {
     if (!c || F < 0 || (F > 0 && (!d_in || !d_bits || !d_valid))) return QPSK_EINVAL;
+    if (c->asm_left > 0) return QPSK_EINVAL;   // channels not yet loaded (qpsk_rx_state_load)
     if (F == 0) return QPSK_OK;
     if ((reinterpret_cast<uintptr_t>(d_in) & 15u) != 0) return QPSK_EINVAL;  // int4 loads
     HCHECK(hipSetDevice(c->device));
@@ -2521,6 +2598,7 @@ extern "C" int qpsk_rx_sync(qpsk_ctx* c) {
     int e = 0;
     HCHECK(hipMemcpyAsync(&e, c->d_err + 1, sizeof e, hipMemcpyDeviceToHost, c->stream));
     HCHECK(hipStreamSynchronize(c->stream));
+    if (e != 0) c->stalled = true;
     return e == 0 ? QPSK_OK : QPSK_ESTALL;
 }
 
@@ -2604,6 +2682,7 @@ static int stage_grow(qpsk_ctx* c, size_t F) {
 extern "C" int qpsk_rx_batch(qpsk_ctx* c, const int16_t* in, int F, uint8_t* bits, uint8_t* valid,
                              int32_t* trace, float* soft) {
     if (!c || F < 0 || (F > 0 && (!in || !bits || !valid))) return QPSK_EINVAL;
+    if (c->asm_left > 0) return QPSK_EINVAL;   // channels not yet loaded (qpsk_rx_state_load)
     if (F == 0) return QPSK_OK;
     HCHECK(hipSetDevice(c->device));
     int r = stage_grow(c, (size_t)F);
@@ -2637,6 +2716,7 @@ extern "C" int qpsk_rx_batch(qpsk_ctx* c, const int16_t* in, int F, uint8_t* bit
         if (soft) memcpy(soft, h + g.soft, nso);
         int e;
         memcpy(&e, h + g.err, sizeof e);
+        if (e != 0) c->stalled = true;
         return e != 0 ? QPSK_ESTALL : QPSK_OK;
     }
     if (pin) memcpy(h + g.in, in, nin);
@@ -2672,6 +2752,7 @@ extern "C" int qpsk_rx_batch(qpsk_ctx* c, const int16_t* in, int F, uint8_t* bit
     if (soft) memcpy(soft, h + g.soft, nso);
     int e;
     memcpy(&e, h + g.err, sizeof e);
+    if (e != 0) c->stalled = true;
     return e != 0 ? QPSK_ESTALL : QPSK_OK;
 }
 

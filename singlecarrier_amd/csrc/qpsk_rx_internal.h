@@ -21,6 +21,9 @@ int* qpsk_rx_err_word(qpsk_ctx* c);
 // Bumped by every qpsk_rx_reset(): a stream keeps reporting a stall for every
 // later chunk until the per-channel state it corrupted has been reset.
 uint64_t qpsk_rx_epoch(const qpsk_ctx* c);
+// A stream chunk of epoch `epoch` stalled: if no reset has run since, the
+// context's per-channel state is undefined (qpsk_rx_state_save refuses it).
+void qpsk_rx_mark_stalled(qpsk_ctx* c, uint64_t epoch);
 
 // The stream that owns a context (qpsk_stream_create_mode): qpsk_rx_reset()
 // and qpsk_rx_state_load() refuse with QPSK_EBUSY while it has chunks pending.

@@ -211,6 +211,7 @@ extern "C" int qpsk_stream_retrieve(qpsk_stream* s, const uint8_t** bits, const 
     if (*q.h_err != 0) {
         s->stalled = true;
         s->stall_epoch = q.epoch;
+        qpsk_rx_mark_stalled(s->rx, q.epoch);   // the context's state too (qpsk_rx_state_save)
     }
     return (s->stalled && q.epoch == s->stall_epoch) ? QPSK_ESTALL : QPSK_OK;
 }

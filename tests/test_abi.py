@@ -157,3 +157,15 @@ def test_fft_alloc_rejects_unsupported_sizes():
         err = C.c_int(0)
         assert not sc.lib().qpsk_fft_alloc(0, n, 0, C.byref(err))
         assert err.value == -1
+
+
+def test_state_load_rejects_short_or_foreign_buffers():
+    """Receiver.state_load checks a snapshot's length and magic before reading
+    its header (a short or foreign buffer is QPSK_EINVAL, not a numpy error);
+    no context is touched, so no GPU is needed."""
+    rx = sc.Receiver.__new__(sc.Receiver)
+    rx._h = None
+    for snap in (b"", b"QPSKSTA1", b"XPSKSTA1" + bytes(120)):
+        with pytest.raises(sc.QpskError) as ei:
+            rx.state_load(snap)
+        assert ei.value.code == sc.QPSK_EINVAL
