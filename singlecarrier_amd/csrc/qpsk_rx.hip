@@ -81,9 +81,6 @@ constexpr int kDec = 296;
 #ifndef QPSK_FIR_WAIT
 #define QPSK_FIR_WAIT 1   // the FIRs: one lgkmcnt(0) per sample batch, not one per sample (0: A/B knob)
 #endif
-#ifndef QPSK_FIR_PIPE
-#define QPSK_FIR_PIPE 0     // the split FIR's LDS batches software-pipelined (fir_pipe; A/B knob)
-#endif
 #ifndef QPSK_FIR_ANCHOR
 // the batched FIRs' accumulators pinned per LDS batch (anchor_f2).  Without it
 // LLVM sinks every multiply-add below the batch's last wait (the FIR ran as
@@ -377,7 +374,7 @@ __device__ __forceinline__ f2 ld2nt(const float2* p) {
     return *(lds_vf2*)p;   // p points into LDS
 }
 // an accumulator pinned in a VGPR at this point of the instruction stream
-// (QPSK_FIR_ANCHOR / QPSK_FIR_PIPE: keeps a batch's arithmetic inside it)
+// (QPSK_FIR_ANCHOR: keeps a batch's arithmetic inside it)
 __device__ __forceinline__ void anchor_f2(f2& y) { asm volatile("" : "+v"(y)); }
 
 #ifdef QPSK_STAMPS
@@ -420,8 +417,10 @@ __device__ __forceinline__ void fir_dec752(int lane, int rt, const float2* M, fl
                     if (s < 69 && k >= 0 && k < QK_NTAPS) y[m] = y[m] + v[j] * QK_RRC[k];
                 }
             }
-            if (QPSK_FIR_ANCHOR == 2)
+            if (QPSK_FIR_ANCHOR == 2) {
+#pragma unroll
                 for (int m = 0; m < 5; m++) anchor_f2(y[m]);
+            }
         }
 #pragma unroll
         for (int m = 0; m < 5; m++) {
@@ -497,8 +496,10 @@ __device__ __forceinline__ void fir_dec(int lane, int rt, const float2* M, float
                     if (s < 59 && k >= 0 && k < QK_NTAPS) y[m] = y[m] + v[j] * QK_RRC[k];
                 }
             }
-            if (QPSK_FIR_ANCHOR == 2)
+            if (QPSK_FIR_ANCHOR == 2) {
+#pragma unroll
                 for (int m = 0; m < 3; m++) anchor_f2(y[m]);
+            }
         }
 #pragma unroll
         for (int m = 0; m < 3; m++)
@@ -509,48 +510,6 @@ __device__ __forceinline__ void fir_dec(int lane, int rt, const float2* M, float
     }
 }
 
-// Software-pipelined LDS batches (QPSK_FIR_PIPE): NS samples ld(s), s < NS,
-// in batches of FB; batch b+1's loads are issued before batch b is computed,
-// and the wait before batch b leaves exactly batch b+1's loads outstanding
-// (lgkmcnt(n): LDS returns in order, and outstanding scalar loads only make
-// the wait stricter).  mac(s, v) consumes sample s in ascending s: the
-// arithmetic and its order are fir_dec's / fir_one's.
-// anchor() pins the accumulators after each batch (an empty volatile asm that
-// reads and writes them): without it LLVM sinks every multiply-add below the
-// last wait, next to the (conditional) store of the result, and the batches
-// become a chain of load rounds with all the arithmetic after them.
-template <int NS, int FB, int B>
-struct FirPipe {
-    static constexpr int kNB = (NS + FB - 1) / FB;
-    template <typename Ld, typename Mac, typename Anchor>
-    static __device__ __forceinline__ void run(f2 (&v)[2][FB], Ld ld, Mac mac, Anchor anchor) {
-        if constexpr (B < kNB) {
-            constexpr int kNext = (B + 1 < kNB) ? ((NS - (B + 1) * FB) < FB ? NS - (B + 1) * FB : FB) : 0;
-            static_assert(kNext <= 15, "lgkmcnt holds 4 bits");
-#pragma unroll
-            for (int j = 0; j < FB; j++)
-                if ((B + 1) * FB + j < NS) v[(B + 1) & 1][j] = ld((B + 1) * FB + j);
-            __builtin_amdgcn_sched_barrier(0);
-            __builtin_amdgcn_s_waitcnt(0xC07F | (kNext << 8));   // lgkmcnt(kNext)
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int j = 0; j < FB; j++)
-                if (B * FB + j < NS) mac(B * FB + j, v[B & 1][j]);
-            anchor();
-            FirPipe<NS, FB, B + 1>::run(v, ld, mac, anchor);
-        }
-    }
-};
-template <int NS, int FB, typename Ld, typename Mac, typename Anchor>
-__device__ __forceinline__ void fir_pipe(Ld ld, Mac mac, Anchor anchor) {
-    f2 v[2][FB];
-#pragma unroll
-    for (int j = 0; j < FB; j++)
-        if (j < NS) v[0][j] = ld(j);
-    FirPipe<NS, FB, 0>::run(v, ld, mac, anchor);
-}
-
-
 // One FIR output per lane: out = GAIN * sum_k b[k] * RRC[k], k ascending
 // (the same operations in the same order as fir_dec / fir_head_at).
 #ifndef QPSK_FB1
@@ -558,12 +517,6 @@ __device__ __forceinline__ void fir_pipe(Ld ld, Mac mac, Anchor anchor) {
 #endif
 __device__ __forceinline__ f2 fir_one(const float2* b) {
     f2 y = {0.0f, 0.0f};
-    if constexpr (QPSK_FIR_PIPE) {
-        fir_pipe<QK_NTAPS, QPSK_FB1>([&](int s) { return ld2nt(b + s); },
-                                     [&](int s, f2 v) { y = y + v * QK_RRC[s]; },
-                                     [&] { anchor_f2(y); });
-        return y * QK_GAIN;
-    }
 #pragma unroll
     for (int s0 = 0; s0 < QK_NTAPS; s0 += QPSK_FB1) {
         f2 v[QPSK_FB1];
@@ -655,18 +608,6 @@ __device__ __forceinline__ void fir_split(int lane, int rt, const float2* M, flo
     {   // pass 1
         const float2* b = lane < 63 ? M + 15 * lane + rt : M + kM1 + j1;
         f2 y[3] = {{0.0f, 0.0f}, {0.0f, 0.0f}, {0.0f, 0.0f}};
-        if constexpr (QPSK_FIR_PIPE) {
-            fir_pipe<59, QPSK_FB>([&](int s) { return ld2nt(b + s); }, [&](int s, f2 v) {
-#pragma unroll
-                for (int m = 0; m < 3; m++) {
-                    const int k = s - 5 * m;
-                    if (k >= 0 && k < QK_NTAPS) y[m] = y[m] + v * QK_RRC[k];
-                }
-            }, [&] {
-#pragma unroll
-                for (int m = 0; m < 3; m++) anchor_f2(y[m]);
-            });
-        } else
 #pragma unroll
         for (int s0 = 0; s0 < 59; s0 += QPSK_FB) {
             f2 v[QPSK_FB];
@@ -687,8 +628,10 @@ __device__ __forceinline__ void fir_split(int lane, int rt, const float2* M, flo
                     if (s < 59 && k >= 0 && k < QK_NTAPS) y[m] = y[m] + v[j] * QK_RRC[k];
                 }
             }
-            if (QPSK_FIR_ANCHOR >= 1)
+            if (QPSK_FIR_ANCHOR >= 1) {
+#pragma unroll
                 for (int m = 0; m < 3; m++) anchor_f2(y[m]);
+            }
         }
 #pragma unroll
         for (int m = 0; m < 3; m++) {
@@ -742,8 +685,10 @@ __device__ __forceinline__ void fir_head_at(int lane, const float2* H, float2* o
                     if (k >= 0 && k < QK_NTAPS) y[m] = y[m] + v[j] * QK_RRC[k];
                 }
             }
-            if (QPSK_FIR_ANCHOR == 2)
+            if (QPSK_FIR_ANCHOR == 2) {
+#pragma unroll
                 for (int m = 0; m < 2; m++) anchor_f2(y[m]);
+            }
         }
         const f2 o0 = y[0] * QK_GAIN, o1 = y[1] * QK_GAIN;   // one 16-B store
         *reinterpret_cast<float4*>(out + 2 * lane) = make_float4(o0.x, o0.y, o1.x, o1.y);
