@@ -81,9 +81,6 @@ constexpr int kDec = 296;
 #ifndef QPSK_FIR_WAIT
 #define QPSK_FIR_WAIT 1   // the FIRs: one lgkmcnt(0) per sample batch, not one per sample (0: A/B knob)
 #endif
-#ifndef QPSK_FIR_FUSE
-#define QPSK_FIR_FUSE 0   // the split FIR's two passes in one batched loop (fir_split; A/B knob)
-#endif
 #ifndef QPSK_FIR_ANCHOR
 // the batched FIRs' accumulators pinned per LDS batch (anchor_f2).  Without it
 // LLVM sinks every multiply-add below the batch's last wait (the FIR ran as
@@ -607,55 +604,6 @@ __device__ __forceinline__ void fir_split(int lane, int rt, const float2* M, flo
     (void)p2tab;
     constexpr int j1 = 56;
     const int j2 = lane + (lane >= 56 ? 1 : 0) + (lane >= 60 ? 1 : 0);
-#endif
-#if QPSK_FIR_FUSE
-    // passes 1 and 2 in one loop (QPSK_FIR_FUSE): each LDS batch holds pass 1's
-    // next 15 samples and pass 2's next 13, and the four accumulation chains
-    // (3 + 1 per lane) interleave, so a chain's dependent adds are not back to
-    // back (no hazard s_nop between them) and the two passes share 4 waits
-    // instead of 4 + 7.  Every chain still adds its products in tap order.
-    {
-        const float2* b = lane < 63 ? M + 15 * lane + rt : M + kM1 + j1;
-        const float2* b2 = M + kM1 + j2;
-        f2 y[3] = {{0.0f, 0.0f}, {0.0f, 0.0f}, {0.0f, 0.0f}};
-        f2 y2 = {0.0f, 0.0f};
-        constexpr int kF1 = 15, kF2 = 13;   // samples per batch: 59 = 15+15+15+14, 49 = 13+13+13+10
-#pragma unroll
-        for (int bt = 0; bt < 4; bt++) {
-            f2 v[kF1], w[kF2];
-#pragma unroll
-            for (int j = 0; j < kF1; j++)
-                if (kF1 * bt + j < 59) v[j] = ld2nt(b + kF1 * bt + j);
-#pragma unroll
-            for (int j = 0; j < kF2; j++)
-                if (kF2 * bt + j < QK_NTAPS) w[j] = ld2nt(b2 + kF2 * bt + j);
-            __builtin_amdgcn_sched_barrier(0);
-            __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int j = 0; j < kF1; j++) {
-                const int s = kF1 * bt + j;
-#pragma unroll
-                for (int m = 0; m < 3; m++) {
-                    const int k = s - 5 * m;
-                    if (s < 59 && k >= 0 && k < QK_NTAPS) y[m] = y[m] + v[j] * QK_RRC[k];
-                }
-                if (j < kF2 && kF2 * bt + j < QK_NTAPS) y2 = y2 + w[j] * QK_RRC[kF2 * bt + j];
-            }
-#pragma unroll
-            for (int m = 0; m < 3; m++) anchor_f2(y[m]);
-            anchor_f2(y2);
-        }
-#pragma unroll
-        for (int m = 0; m < 3; m++) {
-            const f2 o = y[m] * QK_GAIN;
-            const int d = lane < 63 ? 3 * lane + m : QK_NDEC + j1 + 5 * m;
-            if (d < QK_NDEC || lane == 63) dec[d] = make_float2(o.x, o.y);
-        }
-        const f2 o = y2 * QK_GAIN;
-        dec[QK_NDEC + j2] = make_float2(o.x, o.y);
-    }
-    return;
 #endif
     {   // pass 1
         const float2* b = lane < 63 ? M + 15 * lane + rt : M + kM1 + j1;
