@@ -57,7 +57,7 @@ def build(verbose: bool = False) -> str:
 # the receive kernels' sources and build rules, in the order the Makefile's KSRC
 # hashes them (csrc/Makefile: qpsk_kernel_hash())
 KERNEL_SOURCES = ("qpsk_rx.hip", "qpsk_hunt.h", "qpsk_rcp.h", "qpsk_consts.h", "qpsk_fft_dev.h",
-                  "qpsk_fft_tables.h", "qpsk_rx_internal.h", "Makefile")
+                  "qpsk_fft_tables.h", "qpsk_rx_internal.h", "qpsk_split.h", "Makefile")
 
 
 def kernel_source_hash(csrc: str = None) -> str:

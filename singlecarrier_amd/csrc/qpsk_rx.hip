@@ -38,6 +38,7 @@
 #include "qpsk_hunt.h"
 #include "qpsk_rcp.h"
 #include "qpsk_rx_internal.h"
+#include "qpsk_split.h"
 
 #pragma clang fp contract(off)
 
@@ -563,33 +564,13 @@ constexpr int kSplitMi = 255 - (QK_NPRE + QK_NDSYM + 3);   // 93: mi + 162 >= 25
 // LDS cycles per channel in pass 2, none in pass 1 (before this mapping: pass 1
 // lane 63 at F[56] collided for 31 of 32 rt mod 32, and pass 2's j = 64, 65
 // with j = 32, 33 -- profiles/probe/fir_split_banks.py).
+// The map is qpsk_split.h (split_r, split_j1, make_split_tab), checked on the
+// host for every rt by tests/test_split_tab.py.
 // QPSK_SPLIT_BANKS 0: the round-5 mapping (A/B knob).
 #ifndef QPSK_SPLIT_BANKS
 #define QPSK_SPLIT_BANKS 1
 #endif
-__host__ __device__ constexpr int split_r(int rt) { return (15 * 63 + rt - kM1) & 31; }
-__host__ __device__ constexpr int split_j1(int r) { return r <= 24 ? r + 32 : r; }
-struct SplitTab {
-    uint8_t j[32][64];   // [r][lane]: pass 2's output F[j]
-};
-constexpr SplitTab make_split_tab() {
-    SplitTab t{};
-    for (int r = 0; r < 32; r++) {
-        const int j1 = split_j1(r);
-        bool used[67] = {};
-        used[j1] = used[j1 + 5] = used[j1 + 10] = true;
-        for (int i = 0; i < 32; i++) {
-            const int v = 35 + i;
-            const int j = (v == j1 || v == j1 + 5 || v == j1 + 10) ? v - 32 : v;
-            t.j[r][32 + i] = (uint8_t)j;
-            used[j] = true;
-        }
-        int l = 0;
-        for (int v = 0; v < 67; v++)
-            if (!used[v]) t.j[r][l++] = (uint8_t)v;
-    }
-    return t;
-}
+static_assert(kSplitM1 == kM1, "qpsk_split.h: F_{n+1}'s offset in M");
 __constant__ SplitTab kSplitTab = make_split_tab();
 constexpr int kSplitTabWords = QPSK_SPLIT_BANKS ? (int)sizeof(SplitTab) / 4 : 1;
 
