@@ -109,3 +109,51 @@ def test_contexts_from_four_pthreads(tmp_path):
         nb = bits.size
         np.testing.assert_array_equal(got[:nb].reshape(bits.shape), bits, err_msg=f"thread {t}")
         np.testing.assert_array_equal(got[nb:].reshape(valid.shape), valid, err_msg=f"thread {t}")
+
+
+def test_streams_from_three_host_threads():
+    """qpsk_stream objects (each owning its context, pinned slots and three HIP
+    streams) fed from three host threads at once: every chunk sequence equals
+    the oracle over the concatenated frames."""
+    sc.lib()
+    ndev = _devices()
+    jobs = [(91, 150, 4, 5, 7.0, 3), (92, 700, 2, 6, 3.0, 2), (93, 4200, 3, 4, 9.0, 3)]
+    xs = [oracle.synth(s, n, f * k, e) for s, n, f, k, e, _ in jobs]
+    start = threading.Barrier(len(jobs))
+    outs, errs = [None] * len(jobs), [None] * len(jobs)
+
+    def work(t):
+        try:
+            _, nch, fpc, nchunk, _, nslot = jobs[t]
+            x = xs[t]
+            start.wait()
+            st = sc.Stream(nch, fpc, nslot=nslot, device=t % ndev)
+            gb, gv = [], []
+            for k in range(nchunk):
+                st.acquire()[...] = x[:, k * fpc:(k + 1) * fpc]
+                st.submit()
+                if st.pending == nslot:
+                    b, v = st.retrieve()
+                    gb.append(b)
+                    gv.append(v)
+            while st.pending:
+                b, v = st.retrieve()
+                gb.append(b)
+                gv.append(v)
+            st.close()
+            outs[t] = (np.concatenate(gb, axis=1), np.concatenate(gv, axis=1))
+        except BaseException as e:
+            errs[t] = e
+
+    th = [threading.Thread(target=work, args=(t,)) for t in range(len(jobs))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    for t in range(len(jobs)):
+        if errs[t] is not None:
+            raise errs[t]
+        bits, valid, _ = oracle.cpu_rx(xs[t])
+        np.testing.assert_array_equal(outs[t][1], valid, err_msg=f"thread {t}")
+        np.testing.assert_array_equal(outs[t][0], bits, err_msg=f"thread {t}")
+        assert valid.any()
