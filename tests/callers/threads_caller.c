@@ -39,16 +39,16 @@ static void *run(void *arg) {
     uint8_t *pb = malloc(cf * NBITS), *pv = malloc(cf);
     j->rc = -100;
     FILE *f = fopen(j->in, "rb");
-    if (!x || !bits || !valid || !part || !pb || !pv || !f || fread(x, 2, cf * FRAME, f) != cf * FRAME) {
-        if (f) fclose(f);
-        pthread_barrier_wait(&start);
-        return NULL;
-    }
-    fclose(f);
+    const int ok = x && bits && valid && part && pb && pv && f && fread(x, 2, cf * FRAME, f) == cf * FRAME;
+    if (f) fclose(f);
     pthread_barrier_wait(&start);   /* every thread creates its context at once */
     int err = 0;
-    qpsk_ctx *c = qpsk_rx_create_mode(j->device, j->nch, j->mode, &err);
-    if (!c) { j->rc = err; return NULL; }
+    qpsk_ctx *c = ok ? qpsk_rx_create_mode(j->device, j->nch, j->mode, &err) : NULL;
+    if (!c) {
+        if (ok) j->rc = err;
+        free(x); free(bits); free(valid); free(part); free(pb); free(pv);
+        return NULL;
+    }
     /* frames [0, a), [a, b), [b, nf): per-channel state carries across calls */
     const int cut[4] = {0, j->nf / 3, (2 * j->nf) / 3, j->nf};
     int rc = 0;
