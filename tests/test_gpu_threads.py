@@ -157,3 +157,30 @@ def test_streams_from_three_host_threads():
         np.testing.assert_array_equal(outs[t][1], valid, err_msg=f"thread {t}")
         np.testing.assert_array_equal(outs[t][0], bits, err_msg=f"thread {t}")
         assert valid.any()
+
+
+def test_pthreads_under_threadsanitizer(tmp_path):
+    """The same four-pthread run with the library's host code and the caller
+    built with ThreadSanitizer (tests/callers/Makefile `tsan`, ROCm clang; the
+    device code is the product's): no data race is reported, and the outputs
+    still equal the oracle's.  Prebuilt in the build container (skipped when
+    absent)."""
+    exe = os.path.join(ROOT, "tests", "callers", "build", "threads_caller_tsan")
+    if not os.path.exists(exe):
+        pytest.skip("make -C tests/callers tsan")
+    xs = _inputs()
+    args = [exe, str(_devices())]
+    for t, (x, job) in enumerate(zip(xs, JOBS)):
+        x.tofile(tmp_path / f"in{t}.raw")
+        args += [str(tmp_path / f"in{t}.raw"), str(x.shape[0]), str(x.shape[1]), str(job[4]),
+                 str(tmp_path / f"out{t}.bin")]
+    supp = os.path.join(ROOT, "tests", "callers", "tsan.supp")   # the uninstrumented ROCm runtime
+    env = dict(os.environ, TSAN_OPTIONS=f"halt_on_error=1:exitcode=66:report_signal_unsafe=0:suppressions={supp}")
+    r = subprocess.run(args, capture_output=True, text=True, timeout=600, env=env)
+    assert "ThreadSanitizer" not in r.stderr, r.stderr[-6000:]
+    assert r.returncode == 0, r.stderr[-3000:]
+    for t, x in enumerate(xs):
+        bits, valid, _ = oracle.cpu_rx(x, mode=JOBS[t][4])
+        got = np.fromfile(tmp_path / f"out{t}.bin", np.uint8)
+        np.testing.assert_array_equal(got[:bits.size].reshape(bits.shape), bits, err_msg=f"thread {t}")
+        np.testing.assert_array_equal(got[bits.size:].reshape(valid.shape), valid, err_msg=f"thread {t}")
