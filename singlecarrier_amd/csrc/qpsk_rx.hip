@@ -82,6 +82,14 @@ constexpr int kDec = 296;
 #ifndef QPSK_FIR_WAIT
 #define QPSK_FIR_WAIT 1   // the FIRs: one lgkmcnt(0) per sample batch, not one per sample (0: A/B knob)
 #endif
+#ifndef QPSK_LATE_YIELD
+// 4x2 fronts: the frame's last K channels at the back wave's issue priority.
+// Since the anchored FIR the back is the frame's last wave (4.4% of a frame
+// alone, profiles/r06_c19_stamps_c3_both.json); K = 2: C3 -0.7% over 12
+// interleaved rounds (10 faster), K = 1 / 4 +-0, K = 8 +2.4%
+// (profiles/r06_ly_ab.txt, r06_ly2_ab.txt); 0: off
+#define QPSK_LATE_YIELD 2
+#endif
 #ifndef QPSK_FIR_ANCHOR
 // the batched FIRs' accumulators pinned per LDS batch (anchor_f2).  Without it
 // LLVM sinks every multiply-add below the batch's last wait (the FIR ran as
@@ -1955,6 +1963,11 @@ __global__ void __launch_bounds__((64 * kWavesOf<G, FP, MODE, DUAL, W, QUAD>),
             for (int c = 0; on && c < nlive; c++) {
                 const int ch = ch0 + c;
                 float2* dcur = decs[f][c % kDecBuf];
+                // QPSK_LATE_YIELD (A/B knob): the last K channels of a frame at
+                // the back wave's issue priority, so the back (the frame's last
+                // wave) gets its share before the fronts reach the barrier
+                if (QPSK_LATE_YIELD > 0 && c == nlive - QPSK_LATE_YIELD && ((a.roles >> 4) & 3) == 1)
+                    __builtin_amdgcn_s_setprio(0);
                 mix<DM, kFr>(lane, pf, g, P, M);
                 STAMP(0);
                 if (c > 0) store_window(lane, pmi, decs[f][(c - 1) % kDecBuf], wout + (size_t)(ch - 1) * kWinStride);
@@ -1974,6 +1987,7 @@ __global__ void __launch_bounds__((64 * kWavesOf<G, FP, MODE, DUAL, W, QUAD>),
             }
             TAIL_ARRIVE();
             __syncthreads();
+            if (QPSK_LATE_YIELD > 0 && ((a.roles >> 4) & 3) == 1) __builtin_amdgcn_s_setprio(2);
             STAMP(7);
         }
         STAMP_FLUSH();
