@@ -92,7 +92,7 @@ def test_contexts_from_four_pthreads(tmp_path):
     libdir = os.path.dirname(sc.LIB_PATH)
     r = subprocess.run(["gcc", "-std=gnu11", "-O2", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
                         os.path.join(ROOT, "tests", "callers", "threads_caller.c"), "-o", exe,
-                        "-L", libdir, "-lqpsk_hip", f"-Wl,-rpath,{libdir}", "-lpthread"],
+                        sc.LIB_PATH, f"-Wl,-rpath,{libdir}", "-lpthread"],   # QPSK_LIB: any file name
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
     xs = _inputs()

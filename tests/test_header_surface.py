@@ -30,7 +30,7 @@ def _build(tmp_path, include, extra=()):
     cmd = ["gcc", "-std=gnu11", "-O2", "-Wall", "-Werror", "-I", include, CALLER, "-o", exe, *extra]
     if not extra:
         libdir = os.path.dirname(sc.LIB_PATH)
-        cmd += ["-L", libdir, "-lqpsk_hip", f"-Wl,-rpath,{libdir}"]
+        cmd += [sc.LIB_PATH, f"-Wl,-rpath,{libdir}"]   # QPSK_LIB: any file name
     cmd += ["-lm"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
