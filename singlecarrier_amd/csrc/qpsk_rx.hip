@@ -128,19 +128,6 @@ constexpr int kDec = 296;
 // profiles/r03_dynprio_ab.txt); 0: off; 2: every dual-chain shape (A/B knob)
 #define QPSK_DYNPRIO 1
 #endif
-#ifndef QPSK_QSPLIT
-// quad backs at W = 32: each back wave split into a gain wave (the Kalman gain
-// chain, kalman_calculate) and an equalizer wave (the filter, the error and the
-// taps' update) joined by an LDS ring, in a 1x4 shape (4 fronts, 8 back waves);
-// 0: one wave per quad back (A/B knob)
-#define QPSK_QSPLIT 0
-#endif
-#ifndef QPSK_QSPLIT16
-#define QPSK_QSPLIT16 0   // with QPSK_QSPLIT: W = 16 too, as 1x4 (A/B knob)
-#endif
-#ifndef QPSK_QEQ_PRIO
-#define QPSK_QEQ_PRIO 0   // issue priority of QPSK_QSPLIT's equalizer waves (A/B knob)
-#endif
 
 constexpr int kM1 = 1240;
 template <int MODE> struct Cfg;
@@ -249,11 +236,6 @@ __device__ __forceinline__ void spin_wait(int* p, int v, int* err, int* dead,
         __builtin_amdgcn_s_sleep(1);
     }
     if (it == bound && __lane_id() == 0) {
-#ifdef QPSK_STALL_PRINT
-        if (bound == kSpinBound)
-            printf("stall blk %d wave %d lds %u need %d have %d\n", (int)blockIdx.x, (int)(threadIdx.x >> 6),
-                   (unsigned)(uintptr_t)p, v, __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-#endif
         __hip_atomic_store(dead, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         atomicOr(err, kErrStall);
     }
@@ -1285,12 +1267,9 @@ __device__ __forceinline__ f2 mul_dc(f2 f, f2 dd) {
 // reciprocal operand (xso, lane c: xs[c+1], nondecreasing in j, and >= xs[0]
 // >= E unless NaN); the caller tests bmax <= bits(2^125) once per frame, which
 // is qk_rcp_in_range() for every step (a NaN or -x has larger bits).
-// GAIN (QPSK_QSPLIT): the gain chain alone -- no filter, error or tap update
-// (those run in qstep_eq on the equalizer wave); `sl` gets what qstep_eq needs
-// of this step: row c's final gain G and, lane 3, column 4's g, else y[4].
-template <bool EXACT, bool GAIN = false>
+template <bool EXACT>
 __device__ __forceinline__ float qstep(QKal& k, const f2& X0, const f2& X1, const f2& X2, const f2& X3,
-                                       const f2& X4, float ref, int c, unsigned& bmax, float4& sl) {
+                                       const f2& X4, float ref, int c, unsigned& bmax) {
     const float E = QK_KAL_E, q = QK_KAL_Q;
     // 1 where row c has column c+d (d = 2, 3, 4), else 0: h of a missing
     // column is multiplied by 0, so the padding entries of R stay +0
@@ -1299,21 +1278,17 @@ __device__ __forceinline__ float qstep(QKal& k, const f2& X0, const f2& X1, cons
     // reference's 0 + x[0]*eq[0] only differs from x[0]*eq[0] in the sign of a
     // zero, which no output observes, so the chain starts with
     // the broadcast itself
-    float vr = 0.0f, vi = 0.0f, er = 0.0f;
-    if constexpr (!GAIN) {
-        const f2 p = cmul(X1, k.eqr);         // lane c: x[c] * eq[c]
-        const f2 p4 = cmul(X0, k.eq4);        // lane 3: x[4] * eq[4]
-        // (the empty asm keeps the two components scalar adds, so each folds its
-        // DPP source into one v_add_f32_dpp instead of two moves and a packed add)
-        vr = qdf<qd::kB0>(p.x);
-        vi = qdf<qd::kB0>(p.y);
+    const f2 p = cmul(X1, k.eqr);         // lane c: x[c] * eq[c]
+    const f2 p4 = cmul(X0, k.eq4);        // lane 3: x[4] * eq[4]
+    // (the empty asm keeps the two components scalar adds, so each folds its
+    // DPP source into one v_add_f32_dpp instead of two moves and a packed add)
+    float vr = qdf<qd::kB0>(p.x), vi = qdf<qd::kB0>(p.y);
 #define QV(CT, P)                                                   \
     vr = vr + qdf<CT>(P.x); vi = vi + qdf<CT>(P.y);                 \
     asm("" : "+v"(vr), "+v"(vi))
-        QV(qd::kB1, p); QV(qd::kB2, p); QV(qd::kB3, p); QV(qd::kB3, p4);
+    QV(qd::kB1, p); QV(qd::kB2, p); QV(qd::kB3, p); QV(qd::kB3, p4);
 #undef QV
-        er = ref - vr;            // conjf(ref - val) = (ref - vr, vi)
-    }
+    const float er = ref - vr;            // conjf(ref - val) = (ref - vr, vi)
     // column 0 (every lane): f0 = conj(x0), 6.2; g0 = f0 * d0, 6.4; t0 = g0 * f0
     const f2 x0 = qd2<qd::kB0>(X1);
     const f2 g0 = mul_conj_d0(x0, k.dd);
@@ -1387,34 +1362,9 @@ __device__ __forceinline__ float qstep(QKal& k, const f2& X0, const f2& X1, cons
     k.C[2] = qd2<qd::kRot3>(k.R[3]);
     // update_eq: error *= kalman_y (y[4], lane 3); eq[i] += error * conj(g[i])
     const float y4 = qdf<qd::kB3>(yo);
-    if constexpr (GAIN) {
-        sl = c == 3 ? make_float4(G.x, G.y, g.x, g.y) : make_float4(G.x, G.y, y4, y4);
-        return 0.0f;
-    }
     const f2 e = f2{er, vi} * y4;
     k.eqr = k.eqr + cmulc(e, G);     // row c's final gain
     k.eq4 = k.eq4 + cmulc(e, g);     // lane 3: g[4] (row 4 has no updates)
-    return er;
-}
-
-// QPSK_QSPLIT: the equalizer half of qstep on the equalizer wave, from the gain
-// wave's `sl` of the same step: the same operations as qstep's filter (val),
-// error and tap update, on the same operands in the same order.
-__device__ __forceinline__ float qstep_eq(f2& eqr, f2& eq4, const f2& X0, const f2& X1, const float4& sl,
-                                          float ref) {
-    const f2 p = cmul(X1, eqr);
-    const f2 p4 = cmul(X0, eq4);
-    float vr = qdf<qd::kB0>(p.x), vi = qdf<qd::kB0>(p.y);
-#define QV(CT, P)                                                   \
-    vr = vr + qdf<CT>(P.x); vi = vi + qdf<CT>(P.y);                 \
-    asm("" : "+v"(vr), "+v"(vi))
-    QV(qd::kB1, p); QV(qd::kB2, p); QV(qd::kB3, p); QV(qd::kB3, p4);
-#undef QV
-    const float er = ref - vr;
-    const float y4 = qdf<qd::kB2>(sl.z);   // lane 2 carries y[4]
-    const f2 e = f2{er, vi} * y4;
-    eqr = eqr + cmulc(e, f2{sl.x, sl.y});
-    eq4 = eq4 + cmulc(e, f2{sl.z, sl.w});  // lane 3: g[4]
     return er;
 }
 
@@ -1450,9 +1400,8 @@ __device__ __forceinline__ int qtrain(QKal& k, const f2 (&X)[5], const f2* wl, i
         for (int t = 0; t < 8; t++) {
             if ((t & 3) == 0) poll();   // every 4 steps (dynamic priority, rx_kernel kDyn)
             const float ref = ref8[t];
-            float4 sl;
             const float er = qstep<EXACT>(k, w[t & 7], w[(t + 7) & 7], w[(t + 6) & 7], w[(t + 5) & 7],
-                                          w[(t + 4) & 7], ref, c, bmax, sl);
+                                          w[(t + 4) & 7], ref, c, bmax);
             matches += (er * ref > 0.0f) ? 1 : 0;
             w[(t + 4) & 7] = wl[i + t + 4];   // sample of step i+t+4
         }
@@ -1461,14 +1410,25 @@ __device__ __forceinline__ int qtrain(QKal& k, const f2 (&X)[5], const f2* wl, i
     return matches;
 }
 
-// The per-channel outputs of a quad back's frame (back_frame_quad, and the
-// equalizer wave of QPSK_QSPLIT): the decision, the data job of a valid frame
-// (the quad's state gathered by DPP), zero bits of an invalid one, rx_timing.
-template <typename RtFn>
-__device__ __forceinline__ void quad_out(const RxArgs& a, int ch, bool live, int n, int mi, const QKal& k,
-                                         int matches, RtFn get_rt, const f2* wp2, int* rt_next) {
+// back_frame() for a quad per channel: every lane of the quad has the same
+// matches / valid / rt; the quad's lane 0 writes the per-channel outputs.
+template <typename RtFn, typename PollFn>
+__device__ __forceinline__ void back_frame_quad(const RxArgs& a, int ch, bool live, int n, int mi,
+                                                RtFn get_rt, const float2* win, int* rt_next,
+                                                PollFn poll) {
     const int c = lane_id() & 3;
     const bool lead = c == 0;
+    const f2* wp2 = reinterpret_cast<const f2*>(win);
+    QKal k = qkal_reset();
+    f2 X[5];
+    qload_x0(wp2, c, X);
+    bool bad = (a.roles & kForceExact) != 0;
+    int matches = qtrain<false>(k, X, wp2 + c + 2, c, bad, poll);
+    if (__builtin_expect(__ballot(bad) != 0ull, 0)) {   // recompute the frame exactly
+        k = qkal_reset();
+        qload_x0(wp2, c, X);
+        matches = qtrain<true>(k, X, wp2 + c + 2, c, bad, poll);
+    }
     const bool valid = live && matches > QK_MATCH_MIN;   // src/qpsk.c:196
     const size_t cf = (size_t)ch * a.F + n;
     const unsigned long long vm = __ballot(valid && lead);
@@ -1518,182 +1478,6 @@ __device__ __forceinline__ void quad_out(const RxArgs& a, int ch, bool live, int
         if (a.trace)
             *reinterpret_cast<int4*>(a.trace + cf * 4) = make_int4(mi, matches, valid ? 1 : 0, rtn);
     }
-}
-
-// back_frame() for a quad per channel: every lane of the quad has the same
-// matches / valid / rt; the quad's lane 0 writes the per-channel outputs.
-template <typename RtFn, typename PollFn>
-__device__ __forceinline__ void back_frame_quad(const RxArgs& a, int ch, bool live, int n, int mi,
-                                                RtFn get_rt, const float2* win, int* rt_next,
-                                                PollFn poll) {
-    const int c = lane_id() & 3;
-    const f2* wp2 = reinterpret_cast<const f2*>(win);
-    QKal k = qkal_reset();
-    f2 X[5];
-    qload_x0(wp2, c, X);
-    bool bad = (a.roles & kForceExact) != 0;
-    int matches = qtrain<false>(k, X, wp2 + c + 2, c, bad, poll);
-    if (__builtin_expect(__ballot(bad) != 0ull, 0)) {   // recompute the frame exactly
-        k = qkal_reset();
-        qload_x0(wp2, c, X);
-        matches = qtrain<true>(k, X, wp2 + c + 2, c, bad, poll);
-    }
-    quad_out(a, ch, live, n, mi, k, matches, get_rt, wp2, rt_next);
-}
-
-// ------------------------------------------------ quad back, split (QPSK_QSPLIT)
-// The quad step's gain chain (kalman_calculate: 6.2-6.22) needs only the window
-// and the U-D factors, never the taps or the error, so it can run ahead of the
-// equalizer: a gain wave issues qstep<.., GAIN = true> (~22 instructions fewer
-// per step than qstep) and hands each step's gains to an equalizer wave through
-// an LDS ring; the equalizer wave computes the filter, the error and the taps'
-// update (qstep_eq), counts the matches and makes the frame's outputs
-// (quad_out), reading the gain wave's final U-D state from `stage`.  The chain
-// of 128 serial steps per frame is then the gain wave's alone.
-//   gprod: steps written to the ring   econs: steps the equalizer consumed
-//   gpass: passes finished (stage and gbad written)   gbad: the pass must be
-//   redone with IEEE division (back_frame_quad's retrain)
-// Every wait is bounded (spin_wait); the ring holds nring (8 or 16) steps.
-constexpr int kQRing = 16;   // the largest ring (the FFT-hunt kernels' LDS holds 8)
-struct QPair {
-    float4* ring;   // [nring][64]
-    f2* stage;      // [5][64]: R[0..3], dd
-    int* cnt;       // gprod, econs, gpass, gbad
-    int nring;
-};
-
-__device__ __forceinline__ void qwait(int* p, int v, int* err, int* dead) {
-    const int c0 = __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-    if (c0 < v) spin_wait(p, v, err, dead);
-    else __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
-// publish an LDS counter after this wave's LDS stores: the LDS executes one
-// wave's instructions in issue order, so no wait is needed, only the compiler's
-// ordering (a wavefront-scope fence emits no instruction)
-__device__ __forceinline__ void qsignal(int* p, int v) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    if (lane_id() == 0) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-template <bool EXACT, typename PollFn>
-__device__ __forceinline__ void qtrain_gain(QKal& k, const f2 (&X)[5], const f2* wl, int c, bool& bad,
-                                            PollFn poll, const QPair& qp, int& rs, int* err, int* dead) {
-    unsigned bmax = 0u;
-    f2 w[8];
-    w[0] = X[0];
-    w[7] = X[1];
-    w[6] = X[2];
-    w[5] = X[3];
-    w[4] = X[4];
-#pragma unroll
-    for (int t = 1; t < 4; t++) w[t] = wl[t];
-    // the equalizer's count, read 4 steps before it is tested (the LDS
-    // latency off the chain); it lags by ~4 steps, the ring holds 16
-    int ec = __hip_atomic_load(qp.cnt + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    for (int i = 0; i < QK_NPRE; i += 8) {
-        float4* const ring = qp.ring + (i & (qp.nring - 8)) * 64;   // steps rs.. at slot (rs mod nring)
-#pragma unroll
-        for (int t = 0; t < 8; t++) {
-            if ((t & 3) == 0) {
-                poll();
-                // ring slots of steps rs .. rs+3 free
-                if (__builtin_amdgcn_readfirstlane(ec) < rs + 4 - qp.nring) qwait(qp.cnt + 1, rs + 4 - qp.nring, err, dead);
-                ec = __hip_atomic_load(qp.cnt + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
-            float4 sl;
-            (void)qstep<EXACT, true>(k, w[t & 7], w[(t + 7) & 7], w[(t + 6) & 7], w[(t + 5) & 7],
-                                     w[(t + 4) & 7], 0.0f, c, bmax, sl);
-            ring[t * 64 + lane_id()] = sl;
-            w[(t + 4) & 7] = wl[i + t + 4];
-            if ((t & 3) == 3) {
-                rs += 4;
-                qsignal(qp.cnt + 0, rs);
-            }
-        }
-    }
-    if (!EXACT) bad |= bmax > __float_as_uint(0x1p125f);
-}
-
-__device__ __forceinline__ int qtrain_eq(f2& eqr, f2& eq4, const f2* wl, const QPair& qp, int& rc, int* err,
-                                         int* dead) {
-    int matches = 0;
-    f2 w[8];   // w[s mod 8] = x[c+1] of step s (wl[s]); X1 of step s is wl[s-1]
-    w[7] = wl[-1];
-#pragma unroll
-    for (int t = 0; t < 4; t++) w[t] = wl[t];
-    for (int i = 0; i < QK_NPRE; i += 8) {
-        const float4 r0 = *reinterpret_cast<const float4*>(&kPreTab.v[i]);
-        const float4 r1 = *reinterpret_cast<const float4*>(&kPreTab.v[i + 4]);
-        const float ref8[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
-        const float4* const ring = qp.ring + (i & (qp.nring - 8)) * 64;
-#pragma unroll
-        for (int t = 0; t < 8; t++) {
-            if ((t & 3) == 0) qwait(qp.cnt + 0, rc + 4, err, dead);
-            const float4 sl = ring[t * 64 + lane_id()];
-            const float ref = ref8[t];
-            const float er = qstep_eq(eqr, eq4, w[t & 7], w[(t + 7) & 7], sl, ref);
-            matches += (er * ref > 0.0f) ? 1 : 0;
-            w[(t + 4) & 7] = wl[i + t + 4];
-            if ((t & 3) == 3) {
-                rc += 4;
-                qsignal(qp.cnt + 1, rc);
-            }
-        }
-    }
-    return matches;
-}
-
-// the gain wave's frame: one pass, and the exact retrain when the pass's
-// reciprocals left the fast path's range (back_frame_quad)
-template <typename PollFn>
-__device__ __forceinline__ void gain_frame_quad(const RxArgs& a, const float2* win, PollFn poll, const QPair& qp,
-                                                int& rs, int& np, int* dead) {
-    const int c = lane_id() & 3;
-    const f2* wp2 = reinterpret_cast<const f2*>(win);
-    auto pass_end = [&](const QKal& k, bool redo) {
-#pragma unroll
-        for (int i = 0; i < 4; i++) qp.stage[i * 64 + lane_id()] = k.R[i];
-        qp.stage[4 * 64 + lane_id()] = k.dd;
-        if (lane_id() == 0) __hip_atomic_store(qp.cnt + 3, redo ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        qsignal(qp.cnt + 2, ++np);
-    };
-    QKal k = qkal_reset();
-    f2 X[5];
-    qload_x0(wp2, c, X);
-    bool bad = (a.roles & kForceExact) != 0;
-    qtrain_gain<false>(k, X, wp2 + c + 2, c, bad, poll, qp, rs, a.err, dead);
-    const bool redo = __ballot(bad) != 0ull;
-    pass_end(k, redo);
-    if (__builtin_expect(redo, 0)) {
-        k = qkal_reset();
-        qload_x0(wp2, c, X);
-        qtrain_gain<true>(k, X, wp2 + c + 2, c, bad, poll, qp, rs, a.err, dead);
-        pass_end(k, false);
-    }
-}
-
-// the equalizer wave's frame: as many passes as the gain wave made (at most
-// two), then the outputs from the last pass
-template <typename RtFn>
-__device__ __forceinline__ void eq_frame_quad(const RxArgs& a, int ch, bool live, int n, int mi, RtFn get_rt,
-                                              const float2* win, int* rt_next, const QPair& qp, int& rc, int& np,
-                                              int* dead) {
-    const int c = lane_id() & 3;
-    const f2* wp2 = reinterpret_cast<const f2*>(win);
-    QKal k = qkal_reset();
-    int matches = 0;
-    for (int pass = 0; pass < 2; pass++) {
-        k.eqr = k.eq4 = f2{0.0f, 0.0f};
-        matches = qtrain_eq(k.eqr, k.eq4, wp2 + c + 2, qp, rc, a.err, dead);
-        qwait(qp.cnt + 2, ++np, a.err, dead);
-        const int redo = __builtin_amdgcn_readfirstlane(
-            __hip_atomic_load(qp.cnt + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-        if (!redo) break;
-    }
-#pragma unroll
-    for (int i = 0; i < 4; i++) k.R[i] = qp.stage[i * 64 + lane_id()];
-    k.dd = qp.stage[4 * 64 + lane_id()];
-    quad_out(a, ch, live, n, mi, k, matches, get_rt, wp2, rt_next);
 }
 
 // 31 x data_eq + qpsk_demod (src/equalizer.c:64-90, src/qpsk.c:268-271) from
@@ -1827,13 +1611,8 @@ __global__ void __launch_bounds__(256) rx_data_kernel(const float4* jobs, unsign
 //
 // QUAD (DUAL, G == 1 only): the back waves hold a quad of lanes per channel
 // (back_frame_quad), 16 channels per wave, W / 16 waves per frame chain.
-//
-// QPSK_QSPLIT (QUAD with 4 fronts): every quad back is a gain wave and an
-// equalizer wave (gain_frame_quad / eq_frame_quad).
-template <int FP, bool QUAD>
-constexpr bool kQSplitOf = QUAD && QPSK_QSPLIT && FP == 4;
 template <int G, int FP, int MODE, bool DUAL, int W, bool QUAD>
-constexpr int kBackWavesOf = DUAL ? 2 * G * (QUAD ? W / 16 : 1) * (kQSplitOf<FP, QUAD> ? 2 : 1) : G;
+constexpr int kBackWavesOf = DUAL ? 2 * G * (QUAD ? W / 16 : 1) : G;
 
 // waves per SIMD = ceil(waves / 4): 3 (<= 168 VGPRs) for the 12-wave shapes
 template <int G, int FP, int MODE, bool DUAL, int W, bool QUAD>
@@ -1853,8 +1632,6 @@ __global__ void __launch_bounds__((64 * kWavesOf<G, FP, MODE, DUAL, W, QUAD>),
     constexpr int kGroups = G, kFrontPer = FP;
     constexpr int kBackWaves = kBackWavesOf<G, FP, MODE, DUAL, W, QUAD>;
     constexpr int kChainWaves = QUAD ? W / 16 : 1;     // back waves per frame chain and group
-    constexpr bool kQS = kQSplitOf<FP, QUAD>;            // gain + equalizer wave per quad back
-    constexpr int kQP = kQS ? 2 * kChainWaves : 1;       // kQS: gain / equalizer pairs
     constexpr bool kDyn = DUAL && (QPSK_DYNPRIO == 2 || (QPSK_DYNPRIO == 1 && QUAD));
     constexpr int kFrontCh = W / kFrontPer;            // channels per front wave
     constexpr int kFrontWaves = kGroups * kFrontPer;
@@ -1878,10 +1655,6 @@ __global__ void __launch_bounds__((64 * kWavesOf<G, FP, MODE, DUAL, W, QUAD>),
     // DUAL progress counters, per group, frame parity and channel block (one
     // block per back wave of a chain)
     __shared__ int bseq[kGroups][2][kChainWaves], fcnt[kGroups][2][kChainWaves];
-    constexpr int kQR = (MODE & 2) ? 8 : kQRing;           // kQS ring steps
-    __shared__ __attribute__((aligned(16))) float4 qring[kQS ? kQP * kQR * 64 : 1];
-    __shared__ __attribute__((aligned(16))) f2 qstage[kQS ? kQP * 5 * 64 : 1];
-    __shared__ int qcnt[kQS ? kQP * 4 : 1];
     __shared__ int dead_s;                               // DUAL: a wait of this workgroup timed out
     __shared__ int nwait_s;                              // kDyn: back waves waiting for their fronts
 #ifdef QPSK_STAMPS
@@ -1940,7 +1713,6 @@ __global__ void __launch_bounds__((64 * kWavesOf<G, FP, MODE, DUAL, W, QUAD>),
     }
     if (threadIdx.x < 2 * kGroups * kChainWaves) (&bseq[0][0][0])[threadIdx.x] = (&fcnt[0][0][0])[threadIdx.x] = 0;
     if (threadIdx.x == 0) dead_s = nwait_s = 0;
-    if (kQS && threadIdx.x < kQP * 4) qcnt[threadIdx.x] = 0;
     __syncthreads();
     if constexpr (DUAL) {
         // Channel blocks: a group's channels split into one block per back wave
@@ -1959,15 +1731,9 @@ __global__ void __launch_bounds__((64 * kWavesOf<G, FP, MODE, DUAL, W, QUAD>),
         static_assert(kBlkCh % kFrontPer == 0, "block split");
         if (wave < kBackWaves) {
             // ---------------------------------------------------- back of group
-            // gi = (q >> 1) / kChainWaves, block b, frames n = q mod 2; kQS:
-            // waves q < kQP the gain waves, kQP + q their equalizer waves
-            const bool qeq = kQS && wave >= kQP;
-            const int q = kQS ? wave % kQP : wave;
-            const int gi = (q >> 1) / kChainWaves;
-            const int b = (q >> 1) % kChainWaves;
-            const QPair qp{qring + (kQS ? q * kQR * 64 : 0), qstage + (kQS ? q * 5 * 64 : 0),
-                           qcnt + (kQS ? q * 4 : 0), kQR};
-            int qrs = 0, qnp = 0;   // kQS: ring steps and passes of this wave
+            // gi = (wave >> 1) / kChainWaves, block b, frames n = wave mod 2
+            const int gi = (wave >> 1) / kChainWaves;
+            const int b = (wave >> 1) % kChainWaves;
             // channel of this lane within the block: the lane, or its quad.
             // Lanes past the block (lane backs with W < 64) own no channel:
             // they read their block's first channel's slots and write none.
@@ -1976,8 +1742,7 @@ __global__ void __launch_bounds__((64 * kWavesOf<G, FP, MODE, DUAL, W, QUAD>),
             const int idx = kBlkCh * b + (own ? sub : 0);
             const int ch = (grp0 + gi) * W + idx;
             const bool live = own && ch < a.nch;
-            if (qeq) __builtin_amdgcn_s_setprio(QPSK_QEQ_PRIO);
-            else if (kDyn || ((a.roles >> 4) & 3) == 2) __builtin_amdgcn_s_setprio(2);
+            if (kDyn || ((a.roles >> 4) & 3) == 2) __builtin_amdgcn_s_setprio(2);
             // kDyn (QPSK_DYNPRIO): every 4 training steps, drop to the lowest
             // issue priority while another back wave waits for its fronts, else the highest
             auto poll = [&] {
@@ -1995,12 +1760,10 @@ __global__ void __launch_bounds__((64 * kWavesOf<G, FP, MODE, DUAL, W, QUAD>),
             // diagnostic stamps (QPSK_STAMPS): 13 frame work, 14 wait for the
             // fronts, 15 wait for the other chain's decision
             STAMP_DECL
-            for (int n = q & 1; n < a.F; n += 2) {
+            for (int n = wave & 1; n < a.F; n += 2) {
                 const int p = n & 1;
                 // front(n-1) done by every front wave for this block: window n and mi_n
-                if (qeq) {
-                    if (n > 0) spin_wait(&fcnt[gi][p ^ 1][b], kFrontPer * ((n - 1) / 2 + 1), a.err, &dead_s);
-                } else if (n > 0) {
+                if (n > 0) {
                     int* const fc = &fcnt[gi][p ^ 1][b];
                     const int need = kFrontPer * ((n - 1) / 2 + 1);
                     if constexpr (kDyn) {
@@ -2028,13 +1791,7 @@ __global__ void __launch_bounds__((64 * kWavesOf<G, FP, MODE, DUAL, W, QUAD>),
                 };
                 const float2* wn = win_of(a, a.g0 + (unsigned)n) + (size_t)(live ? ch : 0) * kWinStride;
                 int* rtn = own ? &rt_s[gi][p ^ 1][idx] : nullptr;
-                if constexpr (kQS) {
-                    if (!qeq) {   // the decision is the equalizer wave's
-                        gain_frame_quad(a, wn, poll, qp, qrs, qnp, &dead_s);
-                        continue;
-                    }
-                    eq_frame_quad(a, live ? ch : 0, live, n, mi, get_rt, wn, rtn, qp, qrs, qnp, &dead_s);
-                } else if constexpr (QUAD)
+                if constexpr (QUAD)
                     back_frame_quad(a, live ? ch : 0, live, n, mi, get_rt, wn, rtn, poll);
                 else
                     back_frame(a, live ? ch : 0, live, n, mi, get_rt, wn, rtn, poll);
@@ -2136,7 +1893,7 @@ __global__ void __launch_bounds__((64 * kWavesOf<G, FP, MODE, DUAL, W, QUAD>),
                 carry_history<DM>(a.in, a.hist, a.F, bch0(bb), blive(bb), lane);
         }
         __syncthreads();
-        if (wave < (kQS ? kQP : kBackWaves) && (wave & 1) == 0) {   // state after the call's last frame
+        if (wave < kBackWaves && (wave & 1) == 0) {   // state after the call's last frame
             const int gi = (wave >> 1) / kChainWaves;
             const int sub = QUAD ? lane >> 2 : lane;
             const int idx = kBlkCh * ((wave >> 1) % kChainWaves) + sub;
@@ -2800,8 +2557,8 @@ int qpsk_rx_launch(qpsk_ctx* c, const int16_t* d_in, int F, uint8_t* d_bits, uin
         switch (sh.kind) {                                                                     \
             case Shape::k2x4d: QPSK_LAUNCH(2, 4, MM, true, 64, false, HH); break;              \
             case Shape::k1x8d64: QPSK_LAUNCH(1, 8, MM, true, 64, false, HH); break;            \
-            case Shape::k1x8q16: QPSK_LAUNCH(1, (QPSK_QSPLIT && QPSK_QSPLIT16 ? 4 : 8), MM, true, 16, true, HH); break; \
-            case Shape::k1x8q32: QPSK_LAUNCH(1, (QPSK_QSPLIT ? 4 : 8), MM, true, 32, true, HH); break; \
+            case Shape::k1x8q16: QPSK_LAUNCH(1, 8, MM, true, 16, true, HH); break;             \
+            case Shape::k1x8q32: QPSK_LAUNCH(1, 8, MM, true, 32, true, HH); break;             \
             default: QPSK_LAUNCH(4, 2, MM, false, 64, false, HH); break;                       \
         }                                                                                      \
     } while (0)
