@@ -2076,6 +2076,7 @@ struct qpsk_ctx {
     int pend_frames = 0;
     uint64_t epoch = 0;         // qpsk_rx_reset() count (qpsk_rx_epoch)
     int stall_calls = -1;       // QPSK_DEBUG_STALL=first: the stall only in the first launch; -1: every call
+    int short_block = 0;        // QPSK_DEBUG_BLOCK (tests): rx_kernel launched one wave short
     uint64_t launches = 0;      // calls launched over the context's life (qpsk_rx_reset keeps it)
     const qpsk_stream* owner = nullptr;   // the stream this context belongs to, if any
     // a call reported QPSK_ESTALL since the last reset: the per-channel state
@@ -2280,6 +2281,7 @@ extern "C" qpsk_ctx* qpsk_rx_create_mode(int device, int nch, int mode, int* err
         c->roles |= kDebugStall;
         if (!strcmp(ds, "first")) c->stall_calls = 1;           // only the context's first call
     }
+    if (getenv("QPSK_DEBUG_BLOCK")) c->short_block = 64;          // tests: rx_kernel's launch-shape guard
     if (const char* w = getenv("QPSK_WIDTH")) {
         const int v = atoi(w);
         c->width = (v == 16 || v == 32 || v == 64) ? v : 0;
@@ -2544,7 +2546,7 @@ int qpsk_rx_launch(qpsk_ctx* c, const int16_t* d_in, int F, uint8_t* d_bits, uin
 #define QPSK_LAUNCH(GG, FF, MM, DD, WW, QQ, HH)                                                \
     hipLaunchKernelGGL((rx_kernel<GG, FF, MM, DD, WW, QQ, HH>),                                \
                        dim3((unsigned)((c->nch + (size_t)GG * WW - 1) / ((size_t)GG * WW))),   \
-                       dim3(64 * (kBackWavesOf<GG, FF, MM, DD, WW, QQ> + (GG) * (FF))), 0, s,  \
+                       dim3(64 * (kBackWavesOf<GG, FF, MM, DD, WW, QQ> + (GG) * (FF)) - c->short_block), 0, s, \
                        d_in, c->d_hist, c->d_ptab,                                             \
                        c->d_ks, c->d_win[0], c->d_win[1], c->d_mi[0], c->d_mi[1], c->d_rt[0],  \
                        c->d_rt[1], d_bits, d_valid, d_trace, reinterpret_cast<float2*>(d_soft), \

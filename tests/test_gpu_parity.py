@@ -392,6 +392,25 @@ def test_progress_wait_timeout_is_an_error_tiny_call(monkeypatch):
     _vs_oracle(x)
 
 
+@pytest.mark.parametrize("nch", [8, 96, 33000])
+def test_mis_shaped_launch_is_an_error(nch, monkeypatch):
+    """rx_kernel's roles are fixed per instantiation; a launch with a block
+    that does not hold them (QPSK_DEBUG_BLOCK: one wave short) would leave
+    every progress wait to run to its bound.  The kernel refuses it at once:
+    the call reports QPSK_ESTALL (tiny host call, dual-chain and 4x2 shapes),
+    and a new context without the knob is exact."""
+    x = oracle.synth(68, nch, 2, 4.0)
+    monkeypatch.setenv("QPSK_DEBUG_BLOCK", "1")
+    rx = sc.Receiver(nch)
+    with pytest.raises(sc.QpskError) as ei:
+        rx.demod(x)
+    assert ei.value.code == sc.QPSK_ESTALL
+    rx.close()
+    monkeypatch.delenv("QPSK_DEBUG_BLOCK")
+    if nch <= 96:
+        _vs_oracle(x)
+
+
 def test_exact_division_fallback(monkeypatch):
     """The Kalman step's fast reciprocal has an exact-division fallback that
     recomputes a whole frame (rx_kernel) or job (rx_data_kernel) when an
