@@ -320,11 +320,14 @@ def test_head_prepass_c4_shards(nch, monkeypatch):
     _vs_oracle(x)
 
 
+@pytest.mark.parametrize("width", [None, "32"])
 @pytest.mark.parametrize("ebn0", [1000.0, 6.0, 0.0])
-def test_quad_back_edges_and_noise(ebn0):
-    """The quad-per-channel back (160 channels: W = 16) on saturated, zero and
-    constant channels next to noisy ones (sign-of-zero and padding paths of
-    back_frame_quad), every output exact."""
+def test_quad_back_edges_and_noise(ebn0, width, monkeypatch):
+    """The quad-per-channel back (160 channels: W = 16, or W = 32 forced) on
+    saturated, zero and constant channels next to noisy ones (sign-of-zero and
+    padding paths of back_frame_quad), every output exact."""
+    if width:
+        monkeypatch.setenv("QPSK_WIDTH", width)
     x = oracle.synth(71, 160, 9, ebn0)
     x[3] = 0
     x[17] = 32767
@@ -334,10 +337,13 @@ def test_quad_back_edges_and_noise(ebn0):
     _vs_oracle(x)
 
 
-def test_quad_back_exact_division(monkeypatch):
-    """QPSK_FORCE_EXACT on the quad back (100 channels: W = 16): the
-    IEEE-division retrain path."""
+@pytest.mark.parametrize("width", [None, "32"])
+def test_quad_back_exact_division(width, monkeypatch):
+    """QPSK_FORCE_EXACT on the quad back (100 channels: W = 16, or W = 32
+    forced: two back waves per frame chain): the IEEE-division retrain path."""
     monkeypatch.setenv("QPSK_FORCE_EXACT", "1")
+    if width:
+        monkeypatch.setenv("QPSK_WIDTH", width)
     x = oracle.synth(72, 100, 8, 4.0)
     _vs_oracle(x)
 
